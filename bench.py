@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Llama-3-8B bf16 data-parallel training tokens/sec on N MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the driver starts
+one rank per GPU with torchrun.  W untimed warm-up steps, then exactly K timed steps bracketed by
+barrier + device synchronize on both sides; the time is the MAX over ranks; rank 0 prints ONE
+JSON line.  ``value`` is the whole-job tokens/s (all ranks).  Weak scaling: per-GPU batch is
+fixed (micro_batch x seq_len tokens per GPU per step).
+
+Each timed step is the full training step: forward, backward with bucketed RCCL gradient
+all-reduce over xGMI, and the fused AdamW update of all 8.03e9 parameters.
+Data: synthetic random tokens; weights: random init (no network, no checkpoints).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_TOKENS_PER_SEC = None  # the reference publishes no throughput
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default=os.environ.get("TH_BENCH_MODEL", "llama3-8b"))
+    ap.add_argument("--seq-len", type=int, default=int(os.environ.get("TH_BENCH_SEQ", "4096")))
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("TH_BENCH_MB", "4")))
+    ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("TH_BENCH_BUCKET_MB", "256")))
+    args = ap.parse_args()
+
+    import torch
+
+    from tensorhive_fixed_amd.models.llama3 import LlamaConfig
+    from tensorhive_fixed_amd.ops import _lib
+    from tensorhive_fixed_amd.ops.attention import attention_backend
+    from tensorhive_fixed_amd.parallel.dist import init_distributed, shutdown
+    from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer, run_timed
+
+    if torch.cuda.is_available():
+        _lib.load(build_if_missing=True)  # the HIP kernels must be what runs; fail loudly otherwise
+    info = init_distributed()
+    if info.world != args.gpus and info.is_main:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {info.world}", file=sys.stderr)
+    cfg = LlamaConfig.named(args.model)
+    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, 1, bucket_mb=args.bucket_mb)
+    res = run_timed(tr, args.steps, args.warmup)
+    n = info.world
+    flops = cfg.flops_per_token(args.seq_len) * res["tokens_per_sec"]
+    line = {
+        "metric": "llama3_8b_bf16_ddp_train_tokens_per_sec",
+        "value": round(res["tokens_per_sec"], 2),
+        "unit": "tokens/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(res["ms_per_step"], 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None if BASELINE_TOKENS_PER_SEC is None else res["tokens_per_sec"] / BASELINE_TOKENS_PER_SEC,
+        "dtype": "bf16",
+        "data": "synthetic",
+        "config": {
+            "model": "Llama-3-8B" if args.model in ("llama3-8b", "llama3_8b") else args.model,
+            "global_batch": args.micro_batch * n,
+            "seq_len": args.seq_len,
+            "tokens_per_gpu_per_step": args.micro_batch * args.seq_len,
+            "parallelism": f"dp{n}",
+            "optimizer": "AdamW (fp32 master, fused flat kernel, clip 1.0)",
+            "attention": attention_backend(),
+            "grad_bucket_mb": args.bucket_mb,
+        },
+        "tflops_per_gpu": round(flops / n / 1e12, 1),
+        "final_loss": round(res["loss"], 4),
+    }
+    if info.is_main:
+        print(json.dumps(line), flush=True)
+    shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,147 @@
+"""Causal GQA attention on the packed qkv projection (RoPE fused into the same autograd node).
+
+``qkv_attention(qkv, B, S, Hq, Hkv, Dh, theta)`` takes the raw ``[B*S, (Hq + 2*Hkv) * Dh]`` output
+of the fused QKV GEMM, rotates q/k in place (``csrc/rope.hip``), runs causal flash attention
+straight out of that packed buffer (no transposes, no q/k/v copies) and returns
+``o[B*S, Hq*Dh]`` ready for the output projection.  Backward produces ``dqkv`` in the same packed
+layout and applies the inverse rotation in place.
+
+Backends:
+  * ``hip``  -- ``csrc/flash_attn.hip``: MFMA (v_mfma_f32_32x32x16_bf16) flash attention fwd/bwd
+               for gfx950, LSE saved for the backward recompute.  Default on device.
+  * ``sdpa`` -- torch's scaled_dot_product_attention, kept ONLY as an explicitly selected
+               comparison point (``TH_ATTN_BACKEND=sdpa``); never chosen silently.
+  * CPU tensors always use the fp32 math reference.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as Fn
+
+from . import _lib
+from .rope import rope_inplace
+
+
+def attention_backend() -> str:
+    """``TH_ATTN_BACKEND`` if set, else ``hip`` when the flash kernel is in libthk.so."""
+    env = os.environ.get("TH_ATTN_BACKEND")
+    if env:
+        return env
+    try:
+        return "hip" if hasattr(_lib.load(), "th_flash_attn_fwd") else "sdpa"
+    except (RuntimeError, OSError):
+        return "sdpa"
+
+
+def attention_reference(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True) -> torch.Tensor:
+    """fp32 math reference. q [B,S,Hq,D], k/v [B,S,Hkv,D] -> [B,S,Hq,D]."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    rep = Hq // Hkv
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = qf @ kf.transpose(-1, -2) / math.sqrt(D)
+    if causal:
+        m = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(m, float("-inf"))
+    p = s.softmax(-1)
+    return (p @ vf).transpose(1, 2).to(q.dtype)
+
+
+def _split(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int):
+    q = qkv[:, : Hq * Dh].view(B, S, Hq, Dh)
+    k = qkv[:, Hq * Dh: (Hq + Hkv) * Dh].view(B, S, Hkv, Dh)
+    v = qkv[:, (Hq + Hkv) * Dh:].view(B, S, Hkv, Dh)
+    return q, k, v
+
+
+def _sdpa(q, k, v):
+    o = Fn.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                        is_causal=True, enable_gqa=True)
+    return o.transpose(1, 2)
+
+
+def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
+              causal: bool = True) -> tuple[torch.Tensor, torch.Tensor]:
+    """HIP flash attention forward on the packed layout -> (o [B*S, Hq*Dh], lse [B, Hq, S] f32)."""
+    row = qkv.shape[1]
+    if qkv.dtype != torch.bfloat16 or not qkv.is_contiguous() or Dh != 128:
+        raise ValueError("flash kernel needs contiguous bf16 packed qkv and head_dim 128")
+    if Hq % Hkv or row != (Hq + 2 * Hkv) * Dh or qkv.shape[0] != B * S:
+        raise ValueError("flash kernel: inconsistent packed-qkv geometry")
+    o = torch.empty((B * S, Hq * Dh), device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty((B, Hq, S), device=qkv.device, dtype=torch.float32)
+    q = qkv.data_ptr()
+    k = q + Hq * Dh * 2
+    v = k + Hkv * Dh * 2
+    _lib.call("th_flash_attn_fwd", q, k, v, o.data_ptr(), lse.data_ptr(), B, S, Hq, Hkv, Dh,
+              int(causal), row, S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), 0,
+              _lib.stream_ptr(qkv.device))
+    return o, lse
+
+
+def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, B: int,
+              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True) -> torch.Tensor:
+    """HIP flash attention backward -> dqkv in the packed layout."""
+    row = qkv.shape[1]
+    if not do.is_contiguous():
+        do = do.contiguous()
+    dqkv = torch.empty_like(qkv)
+    # f32 dQ accumulator (atomics across key blocks) + delta = rowsum(dO * O) scratch
+    dq_acc = torch.zeros((B * S, Hq * Dh), device=qkv.device, dtype=torch.float32)
+    delta = torch.empty((B, Hq, S), device=qkv.device, dtype=torch.float32)
+    q = qkv.data_ptr()
+    k = q + Hq * Dh * 2
+    v = k + Hkv * Dh * 2
+    dq = dqkv.data_ptr()
+    dk = dq + Hq * Dh * 2
+    dv = dk + Hkv * Dh * 2
+    _lib.call("th_flash_attn_bwd", q, k, v, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+              delta.data_ptr(), dq_acc.data_ptr(), dq, dk, dv, B, S, Hq, Hkv, Dh, int(causal), row,
+              S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), 0, _lib.stream_ptr(qkv.device))
+    return dqkv
+
+
+class _QKVAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B, S, Hq, Hkv, Dh, theta, backend):
+        qkv = qkv if qkv.is_contiguous() else qkv.contiguous()
+        rope_inplace(qkv, S, Hq + Hkv, Dh, theta, 1.0)
+        ctx.dims = (B, S, Hq, Hkv, Dh, theta)
+        ctx.backend = backend
+        if qkv.is_cuda and backend == "hip":
+            o, lse = flash_fwd(qkv, B, S, Hq, Hkv, Dh)
+            ctx.save_for_backward(qkv, o, lse)
+            return o
+        q, k, v = _split(qkv, B, S, Hq, Hkv, Dh)
+        if qkv.is_cuda:
+            o = _sdpa(q, k, v)
+        else:
+            o = attention_reference(q, k, v)
+        ctx.save_for_backward(qkv)
+        return o.reshape(B * S, Hq * Dh)
+
+    @staticmethod
+    def backward(ctx, do):
+        B, S, Hq, Hkv, Dh, theta = ctx.dims
+        if ctx.backend == "hip" and do.is_cuda:
+            qkv, o, lse = ctx.saved_tensors
+            dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh)
+        else:
+            (qkv,) = ctx.saved_tensors
+            with torch.enable_grad():
+                x = qkv.detach().requires_grad_(True)
+                q, k, v = _split(x, B, S, Hq, Hkv, Dh)
+                o = _sdpa(q, k, v) if x.is_cuda else attention_reference(q, k, v)
+                (dqkv,) = torch.autograd.grad(o.reshape(B * S, Hq * Dh), x, do)
+        rope_inplace(dqkv, S, Hq + Hkv, Dh, theta, -1.0)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def qkv_attention(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int, theta: float,
+                  backend: str | None = None) -> torch.Tensor:
+    return _QKVAttention.apply(qkv, B, S, Hq, Hkv, Dh, theta, backend or attention_backend())

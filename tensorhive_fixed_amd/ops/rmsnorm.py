@@ -1,0 +1,84 @@
+"""RMSNorm (Llama) -- HIP kernel on device, fp32 PyTorch reference on CPU.
+
+Kernel: ``csrc/rmsnorm.hip`` (one workgroup per row, row kept in registers, deterministic
+slab-reduced weight gradient).  The weight gradient goes to the flat DDP buffer (``_grad``).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._grad import deliver
+
+
+def rmsnorm_reference(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * r * w.float()).to(x.dtype)
+
+
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, w: torch.Tensor, eps: float):
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        T = x2.shape[0]
+        if x2.is_cuda:
+            if x2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.numel() != D or D % 8:
+                raise ValueError("rmsnorm kernel needs bf16 [T, D] input, bf16 [D] weight, D % 8 == 0")
+            y = torch.empty_like(x2)
+            rstd = torch.empty(T, device=x2.device, dtype=torch.float32)
+            _lib.call("th_rmsnorm_fwd", x2.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr(),
+                      T, D, float(eps), _lib.stream_ptr(x2.device))
+        else:
+            xf = x2.float()
+            rstd = torch.rsqrt(xf.pow(2).mean(-1) + eps)
+            y = (xf * rstd[:, None] * w.float()).to(x2.dtype)
+        ctx.save_for_backward(x2, w, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy: torch.Tensor):
+        x2, w, rstd = ctx.saved_tensors
+        T, D = x2.shape
+        dy2 = dy.reshape(T, D)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        if x2.is_cuda:
+            dx = torch.empty_like(x2)
+            nblk = max(1, min(T, 512))
+            ws = torch.empty(nblk * D, device=x2.device, dtype=torch.float32)
+
+            def run(dw_out: torch.Tensor, accumulate: bool) -> None:
+                _lib.call("th_rmsnorm_bwd", dy2.data_ptr(), x2.data_ptr(), w.data_ptr(),
+                          rstd.data_ptr(), dx.data_ptr(), dw_out.data_ptr(), ws.data_ptr(), nblk, T,
+                          D, int(accumulate), _lib.stream_ptr(x2.device))
+
+            def make() -> torch.Tensor:
+                out = torch.empty_like(w)
+                run(out, False)
+                return out
+
+            gw = deliver(w, run, make)
+            return dx.view(ctx.shape), gw, None
+        xf, gf, wf = x2.float(), dy2.float(), w.float()
+        r = rstd[:, None]
+        dot = (gf * wf * xf).sum(-1, keepdim=True)
+        dx = (r * gf * wf - xf * dot * r.pow(3) / D).to(x2.dtype)
+        dwv = (gf * xf * r).sum(0)
+
+        def write(out: torch.Tensor, accumulate: bool) -> None:
+            if accumulate:
+                out.copy_((out.float() + dwv).to(out.dtype))
+            else:
+                out.copy_(dwv.to(out.dtype))
+
+        gw = deliver(w, write, lambda: dwv.to(w.dtype))
+        return dx.view(ctx.shape), gw, None
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    return _RMSNorm.apply(x, w, eps)

@@ -1,0 +1,87 @@
+"""Process-group bootstrap for one-process-per-GPU jobs (torchrun / th-run launched).
+
+Reads the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT), pins the
+process to its GPU, and initialises ``torch.distributed`` with backend ``nccl`` -- which IS RCCL
+on ROCm, running over xGMI inside an MI355X node -- or ``gloo`` for CPU runs/tests.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int
+    local_rank: int
+    world: int
+    device: torch.device
+    backend: str | None
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def rccl_env_defaults() -> dict[str, str]:
+    """RCCL/HIP environment presets for intra-node xGMI jobs (applied only when unset)."""
+    return {
+        "HSA_ENABLE_IPC_MODE_LEGACY": "0",       # dmabuf IPC (required by this ROCm/driver stack)
+        "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1",  # a dead peer aborts the job instead of hanging
+        "NCCL_DEBUG": "WARN",
+        "TORCH_NCCL_HIGH_PRIORITY": "1",         # comm stream gets priority over compute
+    }
+
+
+def apply_env_defaults() -> None:
+    for k, v in rccl_env_defaults().items():
+        os.environ.setdefault(k, v)
+
+
+def init_distributed(device_type: str | None = None) -> DistInfo:
+    """Initialise from the torchrun environment; single-process when WORLD_SIZE is absent."""
+    apply_env_defaults()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    backend = None
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        backend = "nccl" if device_type == "cuda" else "gloo"
+        kw = {"device_id": device} if device_type == "cuda" else {}
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    elif dist.is_initialized():
+        backend = dist.get_backend()
+    return DistInfo(rank, local_rank, world, device, backend)
+
+
+def barrier(info: DistInfo) -> None:
+    if info.world > 1 and dist.is_initialized():
+        if info.device.type == "cuda":
+            dist.barrier(device_ids=[info.device.index])
+        else:
+            dist.barrier()
+
+
+def max_over_ranks(value: float, info: DistInfo) -> float:
+    if info.world == 1 or not dist.is_initialized():
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=info.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,130 @@
+"""Llama-3 bf16 data-parallel training payload (N07): synthetic tokens, random-init weights.
+
+Launched one process per GPU (``torchrun --nproc_per_node N -m
+tensorhive_fixed_amd.workloads.llama3_ddp``), typically by the tensorhive job queue through the
+``torchrun`` task template with ``HIP_VISIBLE_DEVICES`` taken from the reservation.  It prints
+``[th-train] step=… tokens/s=…`` lines which the daemon's log parser turns into the tokens/s
+reported on the dashboard and in BASELINE.md.
+
+One step = forward + backward (gradient buckets all-reduced over RCCL while backward runs) +
+fused flat AdamW with on-device global-norm clipping.  Nothing is skipped inside a step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+from ..models.llama3 import Llama, LlamaConfig
+from ..parallel.dist import DistInfo, barrier, init_distributed, max_over_ranks, shutdown
+from ..parallel.flat import FlatAdamW, FlatParamStore
+
+
+class SyntheticTokens:
+    """Deterministic per-rank random token batches generated on the device."""
+
+    def __init__(self, vocab: int, batch: int, seq: int, device: torch.device, rank: int, seed: int = 1234):
+        self.vocab, self.batch, self.seq, self.device = vocab, batch, seq, device
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(seed + 7919 * rank)
+
+    def next(self) -> tuple[torch.Tensor, torch.Tensor]:
+        buf = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=self.device,
+                            generator=self.gen)
+        return buf[:, :-1], buf[:, 1:]
+
+
+class Trainer:
+    def __init__(self, cfg: LlamaConfig, info: DistInfo, micro_batch: int, seq_len: int,
+                 grad_accum: int = 1, lr: float = 3e-4, bucket_mb: float = 256.0, seed: int = 0):
+        self.cfg, self.info = cfg, info
+        self.micro_batch, self.seq_len, self.grad_accum = micro_batch, seq_len, grad_accum
+        dev = info.device
+        self.model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
+        self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb)
+        self.opt = FlatAdamW(self.store, lr=lr)
+        self.data = SyntheticTokens(cfg.vocab_size, micro_batch, seq_len, dev, info.rank)
+        self.tokens_per_step = micro_batch * seq_len * grad_accum  # per rank
+        self.last_loss: torch.Tensor | None = None
+
+    def step(self) -> torch.Tensor:
+        n_valid = self.micro_batch * self.seq_len
+        loss_acc = None
+        for mb in range(self.grad_accum):
+            tokens, targets = self.data.next()
+            self.store.begin_microbatch(accumulate=mb > 0, sync=mb == self.grad_accum - 1)
+            loss = self.model(tokens, targets, n_valid=n_valid * self.grad_accum)
+            loss.backward()
+            loss_acc = loss.detach() if loss_acc is None else loss_acc + loss.detach()
+        self.store.finish_grad_sync()
+        self.opt.step()
+        self.last_loss = loss_acc
+        return loss_acc
+
+
+def sync_device(info: DistInfo) -> None:
+    if info.device.type == "cuda":
+        torch.cuda.synchronize(info.device)
+
+
+def run_timed(trainer: Trainer, steps: int, warmup: int) -> dict:
+    info = trainer.info
+    for _ in range(warmup):
+        trainer.step()
+    sync_device(info)
+    barrier(info)
+    sync_device(info)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step()
+    sync_device(info)
+    barrier(info)
+    sync_device(info)
+    dt = max_over_ranks(time.perf_counter() - t0, info)
+    loss = float(trainer.last_loss) if trainer.last_loss is not None else float("nan")
+    toks = trainer.tokens_per_step * info.world * steps
+    return {"seconds": dt, "ms_per_step": 1000.0 * dt / max(1, steps), "tokens_per_sec": toks / dt,
+            "loss": loss}
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description="Llama-3 bf16 DDP training on MI355X (synthetic data)")
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=4)
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-every", type=int, default=1)
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    args = ap.parse_args(argv)
+    info = init_distributed()
+    cfg = LlamaConfig.named(args.model)
+    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb)
+    for _ in range(args.warmup):
+        tr.step()
+    sync_device(info)
+    t_last = time.perf_counter()
+    for s in range(1, args.steps + 1):
+        tr.step()
+        if s % args.log_every == 0:
+            sync_device(info)
+            now = time.perf_counter()
+            dt = max_over_ranks(now - t_last, info)
+            t_last = now
+            tps = tr.tokens_per_step * info.world * args.log_every / dt
+            if info.is_main:
+                print(f"[th-train] step={s} loss={float(tr.last_loss):.4f} tokens/s={tps:.1f} "
+                      f"world={info.world}", flush=True)
+    if info.is_main:
+        print(json.dumps({"event": "done", "steps": args.steps}), flush=True)
+    shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
