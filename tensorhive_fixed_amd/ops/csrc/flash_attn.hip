@@ -1,0 +1,484 @@
+// Causal GQA flash attention, head_dim 128, bf16 in / f32 accumulate, for gfx950 (MI355X).
+//
+// All three kernels read q/k/v straight out of the packed QKV projection output
+// ([tokens, (Hq + 2*Hkv) * 128], row stride `ld`), so the model never transposes or copies.
+// Matrix work is v_mfma_f32_32x32x16_bf16 throughout; the operand orientation is chosen so the
+// softmax statistics are lane-local:
+//
+//   forward  (query-centric, 4 waves x 32 queries per workgroup, 64-key tiles):
+//     S^T = K Q^T        A = K rows (LDS, ds_read_b128)    B = Q rows (registers)
+//     O^T += V^T P^T     A = V^T    (LDS, ds_read_b64_tr_b16)  B = P^T straight from the S^T
+//                        accumulator (query on the lane -> running max / sum need no shuffles
+//                        except one lane^32 exchange, and the O^T rescale is per-lane).
+//   dQ       (query-centric, same skeleton):  S^T, dP^T = V dO^T, dS^T = P^T (dP^T - delta),
+//            dQ^T += K^T dS^T  (K^T via transposed LDS reads).  No atomics: deterministic.
+//   dK/dV    (key-centric, 4 waves x 32 keys, loops over the GQA group's query heads):
+//            S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS.
+//
+// Every LDS tile uses ONE image that serves both 16-byte row reads and transposed reads
+// conflict-free: 256-byte rows, 16-byte chunk index XOR ((row&3)<<2 | (row>>2)&3).
+// Workgroup ids are remapped so each XCD (own L2) gets a contiguous range of the logical order
+// (the GQA query heads that share a K/V head land on one XCD); causal blocks go heaviest first.
+#include "th_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+
+namespace {
+constexpr int HD = 128;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return (row << 8) + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+__device__ __forceinline__ bf16x8 as_bf(ushort8 u) { return __builtin_bit_cast(bf16x8, u); }
+
+__device__ __forceinline__ bf16x8 lds_row(const char* img, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(img + img_off(row, ch));
+}
+
+// Transposed operand (A = X^T with X[row][col] in the image): lane (c = lane&31, h = lane>>5)
+// gets X[rbase + 8*(j>>2) + 4h + (j&3)][cbase + c] in element j (the k order the accumulator
+// -> operand reuse expects).
+__device__ __forceinline__ bf16x8 lds_tr(const char* img, int rbase, int cbase, int lane) {
+  const int h = lane >> 5, grp = (lane >> 4) & 1, i = lane & 15;
+  const int row = rbase + 4 * h + (i >> 2);
+  const int col = cbase + 16 * grp + 4 * (i & 3);
+  const char* p0 = img + img_off(row, col >> 3) + ((col & 7) << 1);
+  const char* p1 = img + img_off(row + 8, col >> 3) + ((col & 7) << 1);
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(p0));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(p1));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[base + j];
+  return r;
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// accumulator row (register r of lane half h) of a 32x32 MFMA tile
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Stage `rows` x 128 bf16 rows (global, row stride ld) into registers: thread t covers row
+// 16*i + (t>>4), 16-byte chunk t&15.  Rows >= limit are zero.
+template <int NP>
+__device__ __forceinline__ void stage_load(ushort8 (&r)[NP], const ushort* base, long ld, int row0,
+                                           int limit, int tid) {
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int row = row0 + 16 * i + (tid >> 4);
+    r[i] = row < limit ? *reinterpret_cast<const ushort8*>(base + (long)row * ld + ((tid & 15) << 3))
+                       : ushort8(0);
+  }
+}
+template <int NP>
+__device__ __forceinline__ void stage_store(char* img, const ushort8 (&r)[NP], int tid) {
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+    *reinterpret_cast<ushort8*>(img + img_off(16 * i + (tid >> 4), tid & 15)) = r[i];
+}
+
+// --------------------------------------------------------------------------------- forward
+constexpr int F_BM = 128, F_BN = 64;
+
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    ushort* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale_log2, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * F_BN * 256];
+  char* ks = smem;
+  char* vs = smem + F_BN * 256;
+  const int nqb = (S + F_BM - 1) / F_BM;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = Hq * B;
+  const int qb = nqb - 1 - L / per;
+  const int rem = L % per;
+  const int b = rem / Hq, hq = rem % Hq, hk = hq / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  const int q0 = qb * F_BM + w * 32;
+  const int q = q0 + c32;
+  const ushort* Qb = Q + b * bs + (long)hq * HD;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    qf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h)
+                        : ushort8(0));
+
+  const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
+  const int ntiles = (kv_end + F_BN - 1) / F_BN;
+  ushort8 kr[4], vr[4];
+  stage_load<4>(kr, Kb, ld, 0, S, tid);
+  stage_load<4>(vr, Vb, ld, 0, S, tid);
+
+  f32x16 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = f32x16(0.f);
+  float m_i = -INFINITY, l_i = 0.f;
+
+  for (int j = 0; j < ntiles; ++j) {
+    __syncthreads();
+    stage_store<4>(ks, kr, tid);
+    stage_store<4>(vs, vr, tid);
+    __syncthreads();
+    if (j + 1 < ntiles) {
+      stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
+      stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
+    }
+    const int kbase = j * F_BN;
+    if (causal && kbase > q0 + 31) continue;  // wave-uniform: tile entirely above the diagonal
+    f32x16 sacc[2] = {f32x16(0.f), f32x16(0.f)};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) sacc[kb] = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc[kb]);
+    }
+    const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float t = sacc[kb][r] * scale_log2;
+        if (need_mask) {
+          const int key = kbase + 32 * kb + acc_row(r, h);
+          if (key >= S || (causal && key > q)) t = -INFINITY;
+        }
+        sacc[kb][r] = t;
+        mt = fmaxf(mt, t);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_i, mt);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_i - m_use);
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(sacc[kb][r] - m_use);
+        sacc[kb][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l_i = l_i * alpha + rs;
+    m_i = m_new;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    bf16x8 pf[4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      pf[2 * kb] = pack8(sacc[kb], 0);
+      pf[2 * kb + 1] = pack8(sacc[kb], 8);
+    }
+#pragma unroll
+    for (int ks4 = 0; ks4 < 4; ++ks4)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d] = mfma(lds_tr(vs, 16 * ks4, 32 * d, lane), pf[ks4], o[d]);
+  }
+
+  if (q < S) {
+    const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
+    ushort* orow = O + b * bso + (long)q * ldo + (long)hq * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4v out;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[e] = f2bf(o[d][4 * g + e] * inv_l);
+        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = out;
+      }
+    if (h == 0) LSE[((long)b * Hq + hq) * S + q] = (m_i + log2f(l_i)) * LN2;
+  }
+}
+
+// ------------------------------------------------------------------------ delta = rowsum(dO*O)
+__global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict__ O,
+                                                       const ushort* __restrict__ dO,
+                                                       float* __restrict__ delta, int B, int S,
+                                                       int Hq, long ldo, long bso) {
+  const long row = blockIdx.x * 16L + (threadIdx.x >> 4);  // (b, q, hq) flattened, 16 lanes/row
+  const long total = (long)B * S * Hq;
+  if (row >= total) return;
+  const int hq = (int)(row % Hq);
+  const long bq = row / Hq;
+  const int q = (int)(bq % S), b = (int)(bq / S);
+  const long off = b * bso + (long)q * ldo + (long)hq * HD + ((threadIdx.x & 15) << 3);
+  const ushort8 a = *reinterpret_cast<const ushort8*>(O + off);
+  const ushort8 g = *reinterpret_cast<const ushort8*>(dO + off);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(g[j]);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  if ((threadIdx.x & 15) == 0) delta[((long)b * Hq + hq) * S + q] = s;
+}
+
+// ------------------------------------------------------------------------------- dQ kernel
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dQ, int B, int S, int Hq, int Hkv, long ld, long bs, long ldo, long bso,
+    float scale, float scale_log2, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * F_BN * 256];
+  char* ks = smem;
+  char* vs = smem + F_BN * 256;
+  const int nqb = (S + F_BM - 1) / F_BM;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = Hq * B;
+  const int qb = nqb - 1 - L / per;
+  const int rem = L % per;
+  const int b = rem / Hq, hq = rem % Hq, hk = hq / (Hq / Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  const int q0 = qb * F_BM + w * 32;
+  const int q = q0 + c32;
+  const ushort* Qb = Q + b * bs + (long)hq * HD;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+  const ushort* dOb = dO + b * bso + (long)hq * HD;
+
+  bf16x8 qf[8], gf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h) : ushort8(0));
+    gf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(dOb + (long)q * ldo + 16 * s + 8 * h) : ushort8(0));
+  }
+  const long st = ((long)b * Hq + hq) * S;
+  const float lse2 = q < S ? LSE[st + q] * LOG2E : INFINITY;
+  const float dlt = q < S ? Dl[st + q] : 0.f;
+
+  const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
+  const int ntiles = (kv_end + F_BN - 1) / F_BN;
+  ushort8 kr[4], vr[4];
+  stage_load<4>(kr, Kb, ld, 0, S, tid);
+  stage_load<4>(vr, Vb, ld, 0, S, tid);
+  f32x16 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = f32x16(0.f);
+
+  for (int j = 0; j < ntiles; ++j) {
+    __syncthreads();
+    stage_store<4>(ks, kr, tid);
+    stage_store<4>(vs, vr, tid);
+    __syncthreads();
+    if (j + 1 < ntiles) {
+      stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
+      stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
+    }
+    const int kbase = j * F_BN;
+    if (causal && kbase > q0 + 31) continue;
+    const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {  // 32-key halves: keeps only one S^T / dP^T pair live
+      f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sacc = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc);
+        pacc = mfma(lds_row(vs, 32 * kb + c32, 2 * s + h), gf[s], pacc);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = exp2f(sacc[r] * scale_log2 - lse2);
+        if (need_mask) {
+          const int key = kbase + 32 * kb + acc_row(r, h);
+          if (key >= S || (causal && key > q)) p = 0.f;
+        }
+        sacc[r] = p * (pacc[r] - dlt);  // dS^T
+      }
+      const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        dq[d] = mfma(lds_tr(ks, 32 * kb, 32 * d, lane), s0, dq[d]);
+        dq[d] = mfma(lds_tr(ks, 32 * kb + 16, 32 * d, lane), s1, dq[d]);
+      }
+    }
+  }
+  if (q < S) {
+    ushort* row = dQ + b * bs + (long)q * ld + (long)hq * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4v out;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[e] = f2bf(dq[d][4 * g + e] * scale);
+        *reinterpret_cast<ushort4v*>(row + 32 * d + 8 * g + 4 * h) = out;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------- dK/dV kernel
+constexpr int B_BK = 128, B_BQ = 32;
+
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  // K image 32 KB | V image 32 KB | Q tile 8 KB | dO tile 8 KB | lse 128 B | delta 128 B
+  __shared__ __attribute__((aligned(16))) char smem[2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4];
+  char* ks = smem;
+  char* vs = ks + B_BK * 256;
+  char* qs = vs + B_BK * 256;
+  char* gs = qs + B_BQ * 256;
+  float* ls = reinterpret_cast<float*>(gs + B_BQ * 256);
+  float* ds = ls + B_BQ;
+  const int nkb = (S + B_BK - 1) / B_BK;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = Hkv * B;
+  // causal: low key blocks see the most queries -> heaviest first
+  const int kblk = causal ? L / per : nkb - 1 - L / per;
+  const int rem = L % per;
+  const int b = rem / Hkv, hk = rem % Hkv;
+  const int G = Hq / Hkv;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  const int kblk0 = kblk * B_BK;
+  const int k0 = kblk0 + 32 * w;
+  const int key = k0 + c32;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+  {
+    ushort8 r[8];
+    stage_load<8>(r, Kb, ld, kblk0, S, tid);
+    stage_store<8>(ks, r, tid);
+    stage_load<8>(r, Vb, ld, kblk0, S, tid);
+    stage_store<8>(vs, r, tid);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) { dk[d] = f32x16(0.f); dv[d] = f32x16(0.f); }
+
+  const int nqt = (S + B_BQ - 1) / B_BQ;
+  const int qt0 = causal ? kblk0 / B_BQ : 0;
+  const int per_head = nqt - qt0;
+  const int total = G * per_head;
+  ushort8 qr[2], gr[2];
+  float lr = 0.f, dr = 0.f;
+  auto prefetch = [&](int it) {
+    const int hq = hk * G + it / per_head;
+    const int qt = qt0 + it % per_head;
+    stage_load<2>(qr, Q + b * bs + (long)hq * HD, ld, qt * B_BQ, S, tid);
+    stage_load<2>(gr, dO + b * bso + (long)hq * HD, ldo, qt * B_BQ, S, tid);
+    if (tid < B_BQ) {
+      const int qq = qt * B_BQ + tid;
+      const long st = ((long)b * Hq + hq) * S;
+      lr = qq < S ? LSE[st + qq] * LOG2E : INFINITY;
+      dr = qq < S ? Dl[st + qq] : 0.f;
+    }
+  };
+  if (total > 0) prefetch(0);
+  for (int it = 0; it < total; ++it) {
+    __syncthreads();
+    stage_store<2>(qs, qr, tid);
+    stage_store<2>(gs, gr, tid);
+    if (tid < B_BQ) { ls[tid] = lr; ds[tid] = dr; }
+    __syncthreads();
+    const int qt = qt0 + it % per_head;
+    if (it + 1 < total) prefetch(it + 1);
+    const int qbase = qt * B_BQ;
+    if (causal && qbase + B_BQ - 1 < k0) continue;  // all queries of the tile precede our keys
+    f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      sacc = mfma(lds_row(qs, c32, 2 * s + h), lds_row(ks, 32 * w + c32, 2 * s + h), sacc);
+      pacc = mfma(lds_row(gs, c32, 2 * s + h), lds_row(vs, 32 * w + c32, 2 * s + h), pacc);
+    }
+    const bool need_mask = (causal && qbase < k0 + 31) || key >= S;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qr_ = acc_row(r, h);
+      float p = exp2f(sacc[r] * scale_log2 - ls[qr_]);
+      if (need_mask && (key >= S || (causal && key > qbase + qr_))) p = 0.f;
+      sacc[r] = p;
+      pacc[r] = p * (pacc[r] - ds[qr_]);
+    }
+    const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
+    const bf16x8 s0 = pack8(pacc, 0), s1 = pack8(pacc, 8);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dv[d] = mfma(lds_tr(gs, 0, 32 * d, lane), p0, dv[d]);
+      dv[d] = mfma(lds_tr(gs, 16, 32 * d, lane), p1, dv[d]);
+      dk[d] = mfma(lds_tr(qs, 0, 32 * d, lane), s0, dk[d]);
+      dk[d] = mfma(lds_tr(qs, 16, 32 * d, lane), s1, dk[d]);
+    }
+  }
+  if (key < S) {
+    ushort* krow = dK + b * bs + (long)key * ld + (long)hk * HD;
+    ushort* vrow = dV + b * bs + (long)key * ld + (long)hk * HD;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4v ok, ov;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ok[e] = f2bf(dk[d][4 * g + e] * scale);
+          ov[e] = f2bf(dv[d][4 * g + e]);
+        }
+        *reinterpret_cast<ushort4v*>(krow + 32 * d + 8 * g + 4 * h) = ok;
+        *reinterpret_cast<ushort4v*>(vrow + 32 * d + 8 * g + 4 * h) = ov;
+      }
+  }
+}
+}  // namespace
+
+static int check_geom(int B, int S, int Hq, int Hkv, int D, long ld, long ldo) {
+  if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv != 0 || D != HD) return -1;
+  if (ld % 8 != 0 || ldo % 8 != 0) return -1;
+  return 0;
+}
+
+extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                                 int B, int S, int Hq, int Hkv, int D, int causal, long ld, long bs,
+                                 long ldo, long bso, float scale, int flags, hipStream_t s) {
+  (void)flags;
+  if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
+  const long nblk = (long)((S + F_BM - 1) / F_BM) * Hq * B;
+  fa_fwd_kernel<<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                              (ushort*)o, lse, B, S, Hq, Hkv, ld, bs, ldo, bso,
+                                              scale * LOG2E, causal);
+  TH_CHECK_LAUNCH();
+}
+
+extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
+                                 const void* dout, const float* lse, float* delta, float* dq_acc,
+                                 void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv, int D,
+                                 int causal, long ld, long bs, long ldo, long bso, float scale,
+                                 int flags, hipStream_t s) {
+  (void)flags;
+  (void)dq_acc;
+  if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
+  const long rows = (long)B * S * Hq;
+  fa_delta_kernel<<<(unsigned)((rows + 15) / 16), 256, 0, s>>>((const ushort*)o, (const ushort*)dout,
+                                                               delta, B, S, Hq, ldo, bso);
+  const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
+  fa_bwd_dq_kernel<<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                (const ushort*)dout, lse, delta, (ushort*)dq, B, S, Hq,
+                                                Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+  const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;
+  fa_bwd_dkv_kernel<<<(unsigned)nk, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                 (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
+                                                 B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
+                                                 causal);
+  TH_CHECK_LAUNCH();
+}
