@@ -22,6 +22,8 @@ for s in ${TH_STEPS:-tests bench}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench_small) step bench_small 600 python bench.py --model llama3-1b-shape --steps 3 --warmup 1 ;;
     bench) step bench 900 python bench.py --steps ${TH_BENCH_STEPS:-5} --warmup 2 ;;
+    kbench) step kbench 600 python scripts/bench_kernels.py ;;
+    flash) step flash_tests 600 python -m pytest tests/gpu/test_flash_attn_gpu.py -x -q ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
   esac
 done
