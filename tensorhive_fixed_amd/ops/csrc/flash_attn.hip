@@ -16,7 +16,7 @@
 //            S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS.
 //
 // Every LDS tile uses ONE image that serves both 16-byte row reads and transposed reads
-// conflict-free: 256-byte rows, 16-byte chunk index XOR ((row&3)<<2 | (row>>2)&3).
+// conflict-free (8-row x 32-column subtiles, see img_off).
 // Workgroup ids are remapped so each XCD (own L2) gets a contiguous range of the logical order
 // (the GQA query heads that share a K/V head land on one XCD); causal blocks go heaviest first.
 #include "th_common.h"
@@ -31,8 +31,12 @@ constexpr int HD = 128;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
+// 8-row x 32-column subtiles of 512 B.  The 16-byte slot of (row, chunk) inside its 256-B bank
+// row is 4*(row&3) + ((ch&3) ^ ((row>>2)&3)): conflict-free for the ds_read_b128 row operands of
+// 32x32x16 MFMAs and for ds_read_b64_tr_b16 transposed operands, and the loop-varying parts
+// (ch>>2 and row>>3) are pure immediates, so each wave needs only 2 address bases per image.
 __device__ __forceinline__ int img_off(int row, int ch) {
-  return (row << 8) + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+  return ((row >> 3) << 11) + ((ch >> 2) << 9) + ((row & 7) << 6) + (((ch & 3) ^ ((row >> 2) & 3)) << 4);
 }
 
 __device__ __forceinline__ bf16x8 as_bf(ushort8 u) { return __builtin_bit_cast(bf16x8, u); }
@@ -328,15 +332,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 }
 
 // ---------------------------------------------------------------------------- dK/dV kernel
-constexpr int B_BK = 128, B_BQ = 32;
+// 8 waves x 32 keys = 256 keys of one (batch, kv head) per workgroup; the K/V block lives in
+// LDS (128 KB) and is re-read every query tile (the reads are kept in the loop on purpose:
+// hoisting them would cost 64 VGPRs and drop the kernel to one wave per SIMD).
+constexpr int B_BK = 256, B_BQ = 32, B_THREADS = 512;
 
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
+__global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
     long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  // K image 32 KB | V image 32 KB | Q tile 8 KB | dO tile 8 KB | lse 128 B | delta 128 B
-  __shared__ __attribute__((aligned(16))) char smem[2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4];
+  // K image 64 KB | V image 64 KB | Q tile 8 KB | dO tile 8 KB | lse 128 B | delta 128 B
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ks = smem;
   char* vs = ks + B_BK * 256;
   char* qs = vs + B_BK * 256;
@@ -346,8 +353,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
   const int nkb = (S + B_BK - 1) / B_BK;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int per = Hkv * B;
-  // causal: low key blocks see the most queries -> heaviest first
-  const int kblk = causal ? L / per : nkb - 1 - L / per;
+  const int kblk = causal ? L / per : nkb - 1 - L / per;  // causal: low key blocks are heaviest
   const int rem = L % per;
   const int b = rem / Hkv, hk = rem % Hkv;
   const int G = Hq / Hkv;
@@ -358,11 +364,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
   const ushort* Kb = K + b * bs + (long)hk * HD;
   const ushort* Vb = V + b * bs + (long)hk * HD;
   {
-    ushort8 r[8];
-    stage_load<8>(r, Kb, ld, kblk0, S, tid);
-    stage_store<8>(ks, r, tid);
-    stage_load<8>(r, Vb, ld, kblk0, S, tid);
-    stage_store<8>(vs, r, tid);
+    // 256 rows x 16 chunks = 4096 chunks per tensor, 8 per thread (row = 32*i + tid/16)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 32 * i + (tid >> 4), ch = tid & 15;
+      const bool ok = kblk0 + row < S;
+      const long go = (long)(kblk0 + row) * ld + (ch << 3);
+      *reinterpret_cast<ushort8*>(ks + img_off(row, ch)) = ok ? *reinterpret_cast<const ushort8*>(Kb + go) : ushort8(0);
+      *reinterpret_cast<ushort8*>(vs + img_off(row, ch)) = ok ? *reinterpret_cast<const ushort8*>(Vb + go) : ushort8(0);
+    }
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
@@ -372,45 +382,50 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
   const int qt0 = causal ? kblk0 / B_BQ : 0;
   const int per_head = nqt - qt0;
   const int total = G * per_head;
-  ushort8 qr[2], gr[2];
+  // Q/dO tile: 32 rows x 16 chunks = 512 chunks -> one per thread per tensor
+  const int srow = tid >> 4, sch = tid & 15;
+  ushort8 qr, gr;
   float lr = 0.f, dr = 0.f;
   auto prefetch = [&](int it) {
     const int hq = hk * G + it / per_head;
-    const int qt = qt0 + it % per_head;
-    stage_load<2>(qr, Q + b * bs + (long)hq * HD, ld, qt * B_BQ, S, tid);
-    stage_load<2>(gr, dO + b * bso + (long)hq * HD, ldo, qt * B_BQ, S, tid);
+    const int qq0 = (qt0 + it % per_head) * B_BQ;
+    const bool ok = qq0 + srow < S;
+    qr = ok ? *reinterpret_cast<const ushort8*>(Q + b * bs + (long)hq * HD + (long)(qq0 + srow) * ld + (sch << 3)) : ushort8(0);
+    gr = ok ? *reinterpret_cast<const ushort8*>(dO + b * bso + (long)hq * HD + (long)(qq0 + srow) * ldo + (sch << 3)) : ushort8(0);
     if (tid < B_BQ) {
-      const int qq = qt * B_BQ + tid;
+      const int qq = qq0 + tid;
       const long st = ((long)b * Hq + hq) * S;
       lr = qq < S ? LSE[st + qq] * LOG2E : INFINITY;
       dr = qq < S ? Dl[st + qq] : 0.f;
     }
   };
   if (total > 0) prefetch(0);
+  int krow = 32 * w + c32;
   for (int it = 0; it < total; ++it) {
     __syncthreads();
-    stage_store<2>(qs, qr, tid);
-    stage_store<2>(gs, gr, tid);
+    *reinterpret_cast<ushort8*>(qs + img_off(srow, sch)) = qr;
+    *reinterpret_cast<ushort8*>(gs + img_off(srow, sch)) = gr;
     if (tid < B_BQ) { ls[tid] = lr; ds[tid] = dr; }
     __syncthreads();
-    const int qt = qt0 + it % per_head;
+    const int qbase = (qt0 + it % per_head) * B_BQ;
     if (it + 1 < total) prefetch(it + 1);
-    const int qbase = qt * B_BQ;
     if (causal && qbase + B_BQ - 1 < k0) continue;  // all queries of the tile precede our keys
+    asm volatile("" : "+v"(krow));  // keep the K/V row reads inside the loop (see header)
     f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      sacc = mfma(lds_row(qs, c32, 2 * s + h), lds_row(ks, 32 * w + c32, 2 * s + h), sacc);
-      pacc = mfma(lds_row(gs, c32, 2 * s + h), lds_row(vs, 32 * w + c32, 2 * s + h), pacc);
-    }
+    for (int s = 0; s < 8; ++s) sacc = mfma(lds_row(qs, c32, 2 * s + h), lds_row(ks, krow, 2 * s + h), sacc);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) pacc = mfma(lds_row(gs, c32, 2 * s + h), lds_row(vs, krow, 2 * s + h), pacc);
     const bool need_mask = (causal && qbase < k0 + 31) || key >= S;
+    const float* lsh = ls + 4 * h;  // one base per lane; the row offsets below are immediates
+    const float* dsh = ds + 4 * h;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int qr_ = acc_row(r, h);
-      float p = exp2f(sacc[r] * scale_log2 - ls[qr_]);
-      if (need_mask && (key >= S || (causal && key > qbase + qr_))) p = 0.f;
+      const int ro = (r & 3) + 8 * (r >> 2);
+      float p = exp2f(sacc[r] * scale_log2 - lsh[ro]);
+      if (need_mask && (key >= S || (causal && key > qbase + ro + 4 * h))) p = 0.f;
       sacc[r] = p;
-      pacc[r] = p * (pacc[r] - ds[qr_]);
+      pacc[r] = p * (pacc[r] - dsh[ro]);
     }
     const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
     const bf16x8 s0 = pack8(pacc, 0), s1 = pack8(pacc, 8);
@@ -418,13 +433,16 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
     for (int d = 0; d < 4; ++d) {
       dv[d] = mfma(lds_tr(gs, 0, 32 * d, lane), p0, dv[d]);
       dv[d] = mfma(lds_tr(gs, 16, 32 * d, lane), p1, dv[d]);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
       dk[d] = mfma(lds_tr(qs, 0, 32 * d, lane), s0, dk[d]);
       dk[d] = mfma(lds_tr(qs, 16, 32 * d, lane), s1, dk[d]);
     }
   }
   if (key < S) {
-    ushort* krow = dK + b * bs + (long)key * ld + (long)hk * HD;
-    ushort* vrow = dV + b * bs + (long)key * ld + (long)hk * HD;
+    ushort* krow_o = dK + b * bs + (long)key * ld + (long)hk * HD;
+    ushort* vrow_o = dV + b * bs + (long)key * ld + (long)hk * HD;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
@@ -435,11 +453,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkv_kernel(
           ok[e] = f2bf(dk[d][4 * g + e] * scale);
           ov[e] = f2bf(dv[d][4 * g + e]);
         }
-        *reinterpret_cast<ushort4v*>(krow + 32 * d + 8 * g + 4 * h) = ok;
-        *reinterpret_cast<ushort4v*>(vrow + 32 * d + 8 * g + 4 * h) = ov;
+        *reinterpret_cast<ushort4v*>(krow_o + 32 * d + 8 * g + 4 * h) = ok;
+        *reinterpret_cast<ushort4v*>(vrow_o + 32 * d + 8 * g + 4 * h) = ov;
       }
   }
 }
+constexpr int B_LDS = 2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4;
 }  // namespace
 
 static int check_geom(int B, int S, int Hq, int Hkv, int D, long ld, long ldo) {
@@ -476,7 +495,12 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
                                                 (const ushort*)dout, lse, delta, (ushort*)dq, B, S, Hq,
                                                 Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
   const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;
-  fa_bwd_dkv_kernel<<<(unsigned)nk, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, B_LDS);
+    attr_set = true;
+  }
+  fa_bwd_dkv_kernel<<<(unsigned)nk, B_THREADS, B_LDS, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                  (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
                                                  B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
                                                  causal);
