@@ -1,0 +1,86 @@
+"""Build the native (non-kernel) components in-tree: ``python -m tensorhive_fixed_amd.native.build``.
+
+Targets (all into ``native/bin`` / ``native/lib``; git-ignored, shipped with the repo snapshot):
+  * ``bin/th-run``        -- C++ task supervisor (replaces GNU screen)              [g++]
+  * ``lib/libthsmi.so``   -- amdsmi telemetry + process attribution (ctypes)        [g++ + libamd_smi]
+  * ``bin/th-smi``        -- CLI / ``--stream`` agent over the same sampler          [g++ + libamd_smi]
+  * ``bin/rccl-bench``    -- RCCL/xGMI collective + direct P2P all-reduce bench      [hipcc + librccl]
+The gfx950 kernels (incl. the th-probe kernel) are built by :mod:`..ops.build` into ``libthk.so``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+BIN = HERE / "bin"
+LIB = HERE / "lib"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+CXX = os.environ.get("CXX", "g++")
+HIPCC = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
+ARCH = os.environ.get("TH_OFFLOAD_ARCH", "gfx950")
+
+TARGETS = {
+    "th-run": (BIN / "th-run", [CXX, "-O2", "-std=c++17", "-Wall", str(HERE / "th_run.cpp")]),
+    "libthsmi": (LIB / "libthsmi.so", [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{ROCM}/include",
+                                       str(HERE / "thsmi.cpp"), f"-L{ROCM}/lib", "-lamd_smi",
+                                       f"-Wl,-rpath,{ROCM}/lib"]),
+    "th-smi": (BIN / "th-smi", [CXX, "-O2", "-std=c++17", "-DTHSMI_MAIN", f"-I{ROCM}/include",
+                                str(HERE / "thsmi.cpp"), f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib"]),
+    "rccl-bench": (BIN / "rccl-bench", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}",
+                                        str(HERE / "rccl_bench.hip"), f"-L{ROCM}/lib", "-lrccl",
+                                        f"-Wl,-rpath,{ROCM}/lib"]),
+}
+
+
+def path_of(name: str) -> Path:
+    return TARGETS[name][0]
+
+
+def _build_one(name: str, force: bool) -> tuple[str, str | None]:
+    out, cmd = TARGETS[name]
+    srcs = [Path(c) for c in cmd if c.endswith((".cpp", ".hip"))]
+    if not force and out.exists() and all(out.stat().st_mtime >= s.stat().st_mtime for s in srcs):
+        return name, None
+    if shutil.which(cmd[0]) is None and not Path(cmd[0]).exists():
+        return name, f"compiler {cmd[0]} not found"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_name(out.name + ".tmp")
+    r = subprocess.run(cmd + ["-o", str(tmp)], capture_output=True, text=True)
+    if r.returncode != 0:
+        return name, r.stderr[-3000:]
+    os.replace(tmp, out)
+    return name, None
+
+
+def build_all(force: bool = False, strict: bool = True) -> dict[str, str | None]:
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        results = dict(ex.map(lambda n: _build_one(n, force), TARGETS))
+    errs = {k: v for k, v in results.items() if v}
+    for k, v in errs.items():
+        print(f"[native] {k}: FAILED\n{v}", file=sys.stderr)
+    if errs and strict:
+        raise RuntimeError(f"native build failed: {sorted(errs)}")
+    return results
+
+
+def th_run_binary() -> str:
+    """Path of the th-run supervisor (built on demand; falls back to PATH)."""
+    p = path_of("th-run")
+    if not p.exists():
+        try:
+            _build_one("th-run", False)
+        except Exception:  # noqa: BLE001
+            pass
+    if p.exists():
+        return str(p)
+    return shutil.which("th-run") or "th-run"
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("[native] built:", ", ".join(str(v[0]) for v in TARGETS.values()))

@@ -1,0 +1,409 @@
+// th-run: the task supervisor that replaces GNU `screen` for tensorhive_fixed_amd.
+//
+// Reference behaviour being replaced (tensorhive/core/task_nursery.py:47-152): tasks were run as
+//   screen -Dm -S tensorhive_task_<id> bash -c "<cmd> |& tee --ignore-interrupts <log>" & echo $!
+// and controlled with `screen -X stuff ^C` / `screen -X quit` / `kill -9` / `screen -ls`.
+//
+//   th-run spawn --name NAME --log FILE [--state-dir DIR] [--env K=V]... [--cwd DIR] -- CMD ARGS...
+//       Detaches (double fork + setsid), starts CMD in its OWN process group with stdout+stderr
+//       on a pipe, and prints the pid of CMD (== its pgid) on stdout, then returns.  A small
+//       monitor process (own session, ignores SIGINT/SIGTERM/SIGHUP like `tee --ignore-interrupts`)
+//       copies the pipe into FILE line by line, reaps CMD and records its exit status.
+//   th-run interrupt|terminate|kill (--name NAME | --pid PID) [--state-dir DIR]
+//       SIGINT / SIGTERM / SIGKILL to the task's whole process group (torchrun + all ranks).
+//   th-run ls [--all] [--state-dir DIR]     one JSON object per session (live ones by default)
+//   th-run status --name NAME               JSON of one session
+//   th-run wait --name NAME [--timeout S]   block until the task exits; exit code = task's
+//
+// State: one `NAME.state` key=value file per session in the state dir (default
+// $TH_RUN_STATE_DIR or ~/.local/state/tensorhive/th-run), written atomically (rename).  These
+// files are the durable PID truth the daemon re-adopts after a restart.
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+namespace {
+
+std::string state_dir_default() {
+  const char* e = getenv("TH_RUN_STATE_DIR");
+  if (e && *e) return e;
+  const char* home = getenv("HOME");
+  return std::string(home ? home : "/tmp") + "/.local/state/tensorhive/th-run";
+}
+
+int mkdirs(const std::string& path) {
+  std::string cur;
+  for (size_t i = 0; i < path.size(); ++i) {
+    cur += path[i];
+    if ((path[i] == '/' && i > 0) || i + 1 == path.size()) {
+      if (mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return -1;
+    }
+  }
+  return 0;
+}
+
+std::string dirname_of(const std::string& p) {
+  size_t k = p.rfind('/');
+  return k == std::string::npos ? "." : (k == 0 ? "/" : p.substr(0, k));
+}
+
+std::string expand_home(const std::string& p) {
+  if (!p.empty() && p[0] == '~') {
+    const char* home = getenv("HOME");
+    return std::string(home ? home : "") + p.substr(1);
+  }
+  return p;
+}
+
+typedef std::map<std::string, std::string> KV;
+
+bool write_state(const std::string& dir, const std::string& name, const KV& kv) {
+  std::string path = dir + "/" + name + ".state";
+  std::string tmp = path + ".tmp." + std::to_string(getpid());
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) return false;
+  for (const auto& it : kv) fprintf(f, "%s=%s\n", it.first.c_str(), it.second.c_str());
+  fflush(f);
+  fsync(fileno(f));
+  fclose(f);
+  return rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+bool read_state(const std::string& path, KV& kv) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char line[8192];
+  while (fgets(line, sizeof line, f)) {
+    char* eq = strchr(line, '=');
+    if (!eq) continue;
+    *eq = 0;
+    std::string v(eq + 1);
+    while (!v.empty() && (v.back() == '\n' || v.back() == '\r')) v.pop_back();
+    kv[line] = v;
+  }
+  fclose(f);
+  return true;
+}
+
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          char b[8];
+          snprintf(b, sizeof b, "\\u%04x", c);
+          o += b;
+        } else {
+          o += (char)c;
+        }
+    }
+  }
+  return o;
+}
+
+bool pid_alive(long pid) {
+  if (pid <= 0) return false;
+  if (kill((pid_t)pid, 0) == 0) return true;
+  return errno == EPERM;
+}
+
+std::string to_json(const KV& kv, bool alive) {
+  std::string o = "{";
+  bool first = true;
+  for (const auto& it : kv) {
+    if (!first) o += ",";
+    first = false;
+    const bool num = it.first == "pid" || it.first == "pgid" || it.first == "monitor_pid" ||
+                     it.first == "exit_code" || it.first == "started" || it.first == "ended";
+    o += "\"" + json_escape(it.first) + "\":";
+    if (num && !it.second.empty())
+      o += it.second;
+    else
+      o += "\"" + json_escape(it.second) + "\"";
+  }
+  o += std::string(first ? "" : ",") + "\"alive\":" + (alive ? "true" : "false") + "}";
+  return o;
+}
+
+void write_all(int fd, const char* p, ssize_t n) {
+  while (n > 0) {
+    ssize_t w = write(fd, p, (size_t)n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return;
+    }
+    p += w;
+    n -= w;
+  }
+}
+
+int usage() {
+  fprintf(stderr,
+          "usage: th-run spawn --name NAME --log FILE [--state-dir D] [--env K=V].. [--cwd D] -- CMD..\n"
+          "       th-run interrupt|terminate|kill (--name NAME | --pid PID) [--state-dir D]\n"
+          "       th-run ls [--all] [--state-dir D] | status --name NAME | wait --name NAME [--timeout S]\n");
+  return 2;
+}
+
+struct Args {
+  std::string cmd, name, log, state_dir, cwd;
+  long pid = -1;
+  double timeout = -1;
+  bool all = false;
+  std::vector<std::string> env;
+  std::vector<std::string> argv;
+};
+
+bool parse(int argc, char** argv, Args& a) {
+  if (argc < 2) return false;
+  a.cmd = argv[1];
+  a.state_dir = state_dir_default();
+  for (int i = 2; i < argc; ++i) {
+    std::string s = argv[i];
+    auto need = [&](std::string& dst) {
+      if (i + 1 >= argc) return false;
+      dst = argv[++i];
+      return true;
+    };
+    if (s == "--") {
+      for (int j = i + 1; j < argc; ++j) a.argv.push_back(argv[j]);
+      break;
+    } else if (s == "--name") {
+      if (!need(a.name)) return false;
+    } else if (s == "--log") {
+      if (!need(a.log)) return false;
+    } else if (s == "--state-dir") {
+      if (!need(a.state_dir)) return false;
+    } else if (s == "--cwd") {
+      if (!need(a.cwd)) return false;
+    } else if (s == "--env") {
+      std::string e;
+      if (!need(e)) return false;
+      a.env.push_back(e);
+    } else if (s == "--pid") {
+      std::string p;
+      if (!need(p)) return false;
+      a.pid = atol(p.c_str());
+    } else if (s == "--timeout") {
+      std::string t;
+      if (!need(t)) return false;
+      a.timeout = atof(t.c_str());
+    } else if (s == "--all") {
+      a.all = true;
+    } else {
+      return false;
+    }
+  }
+  a.state_dir = expand_home(a.state_dir);
+  a.log = expand_home(a.log);
+  return true;
+}
+
+// ------------------------------------------------------------------------------- spawn
+int do_spawn(Args& a) {
+  if (a.name.empty() || a.log.empty() || a.argv.empty()) return usage();
+  if (mkdirs(a.state_dir) != 0 || mkdirs(dirname_of(a.log)) != 0) {
+    perror("th-run: mkdir");
+    return 1;
+  }
+  int hs[2];  // handshake: grandchild command pid back to the caller
+  if (pipe(hs) != 0) return 1;
+  pid_t p1 = fork();
+  if (p1 < 0) return 1;
+  if (p1 > 0) {  // caller: read the command pid, print it, done
+    close(hs[1]);
+    long cpid = -1;
+    ssize_t n = read(hs[0], &cpid, sizeof cpid);
+    close(hs[0]);
+    waitpid(p1, nullptr, 0);
+    if (n != (ssize_t)sizeof cpid || cpid <= 0) {
+      fprintf(stderr, "th-run: spawn failed\n");
+      return 1;
+    }
+    printf("%ld\n", cpid);
+    fflush(stdout);
+    return 0;
+  }
+  // first child -> new session, then fork the monitor so it is not a session leader's child
+  close(hs[0]);
+  setsid();
+  pid_t p2 = fork();
+  if (p2 < 0) _exit(1);
+  if (p2 > 0) _exit(0);
+  // monitor process
+  signal(SIGINT, SIG_IGN);
+  signal(SIGTERM, SIG_IGN);
+  signal(SIGHUP, SIG_IGN);
+  signal(SIGPIPE, SIG_IGN);
+  int out[2];
+  if (pipe(out) != 0) _exit(1);
+  int logfd = open(a.log.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+  if (logfd < 0) _exit(1);
+  pid_t c = fork();
+  if (c < 0) _exit(1);
+  if (c == 0) {  // the task: own process group, default signal dispositions
+    setpgid(0, 0);
+    signal(SIGINT, SIG_DFL);
+    signal(SIGTERM, SIG_DFL);
+    signal(SIGHUP, SIG_DFL);
+    signal(SIGPIPE, SIG_DFL);
+    dup2(out[1], 1);
+    dup2(out[1], 2);
+    close(out[0]);
+    close(out[1]);
+    close(logfd);
+    close(hs[1]);
+    int devnull = open("/dev/null", O_RDONLY);
+    if (devnull >= 0) {
+      dup2(devnull, 0);
+      close(devnull);
+    }
+    for (const auto& e : a.env) putenv(strdup(e.c_str()));
+    if (!a.cwd.empty() && chdir(expand_home(a.cwd).c_str()) != 0) perror("th-run: chdir");
+    std::vector<char*> av;
+    for (auto& s : a.argv) av.push_back(const_cast<char*>(s.c_str()));
+    av.push_back(nullptr);
+    execvp(av[0], av.data());
+    fprintf(stderr, "th-run: exec %s: %s\n", av[0], strerror(errno));
+    _exit(127);
+  }
+  setpgid(c, c);  // race-free: both sides set it
+  close(out[1]);
+  KV st;
+  st["name"] = a.name;
+  st["pid"] = std::to_string((long)c);
+  st["pgid"] = std::to_string((long)c);
+  st["monitor_pid"] = std::to_string((long)getpid());
+  st["started"] = std::to_string((long)time(nullptr));
+  st["log"] = a.log;
+  std::string cmdline;
+  for (auto& s : a.argv) cmdline += (cmdline.empty() ? "" : " ") + s;
+  st["cmd"] = cmdline;
+  st["status"] = "running";
+  write_state(a.state_dir, a.name, st);
+  long cpid = (long)c;
+  write_all(hs[1], (const char*)&cpid, sizeof cpid);
+  close(hs[1]);
+  int devnull = open("/dev/null", O_RDWR);
+  if (devnull >= 0) {
+    dup2(devnull, 0);
+    dup2(devnull, 1);
+    dup2(devnull, 2);
+    close(devnull);
+  }
+  char buf[65536];
+  for (;;) {
+    ssize_t n = read(out[0], buf, sizeof buf);
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) break;
+    write_all(logfd, buf, n);
+  }
+  int wst = 0;
+  while (waitpid(c, &wst, 0) < 0 && errno == EINTR) {
+  }
+  int code = WIFEXITED(wst) ? WEXITSTATUS(wst) : (WIFSIGNALED(wst) ? 128 + WTERMSIG(wst) : -1);
+  st["status"] = "exited";
+  st["exit_code"] = std::to_string(code);
+  st["ended"] = std::to_string((long)time(nullptr));
+  write_state(a.state_dir, a.name, st);
+  close(logfd);
+  _exit(0);
+}
+
+bool lookup(const Args& a, KV& kv) {
+  if (a.name.empty()) return false;
+  return read_state(a.state_dir + "/" + a.name + ".state", kv);
+}
+
+int do_signal(const Args& a, int sig) {
+  long pg = a.pid;
+  if (pg <= 0) {
+    KV kv;
+    if (!lookup(a, kv)) {
+      fprintf(stderr, "th-run: no session %s\n", a.name.c_str());
+      return 3;
+    }
+    if (kv["status"] == "exited") return 4;
+    pg = atol(kv["pgid"].c_str());
+  }
+  if (pg <= 0) return 3;
+  if (kill(-(pid_t)pg, sig) != 0 && kill((pid_t)pg, sig) != 0) {
+    perror("th-run: kill");
+    return 1;
+  }
+  return 0;
+}
+
+int do_ls(const Args& a) {
+  DIR* d = opendir(a.state_dir.c_str());
+  if (!d) return 0;
+  struct dirent* e;
+  while ((e = readdir(d)) != nullptr) {
+    std::string n = e->d_name;
+    if (n.size() < 7 || n.substr(n.size() - 6) != ".state") continue;
+    KV kv;
+    if (!read_state(a.state_dir + "/" + n, kv)) continue;
+    const bool alive = kv["status"] == "running" && pid_alive(atol(kv["pid"].c_str()));
+    if (!alive && !a.all) continue;
+    printf("%s\n", to_json(kv, alive).c_str());
+  }
+  closedir(d);
+  return 0;
+}
+
+int do_status(const Args& a) {
+  KV kv;
+  if (!lookup(a, kv)) return 3;
+  const bool alive = kv["status"] == "running" && pid_alive(atol(kv["pid"].c_str()));
+  printf("%s\n", to_json(kv, alive).c_str());
+  return 0;
+}
+
+int do_wait(const Args& a) {
+  struct timespec t0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (;;) {
+    KV kv;
+    if (!lookup(a, kv)) return 3;
+    if (kv["status"] == "exited") return atoi(kv["exit_code"].c_str());
+    if (!pid_alive(atol(kv["pid"].c_str())) && !pid_alive(atol(kv["monitor_pid"].c_str()))) return 137;
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    const double el = (t.tv_sec - t0.tv_sec) + 1e-9 * (t.tv_nsec - t0.tv_nsec);
+    if (a.timeout >= 0 && el > a.timeout) return 124;
+    usleep(20000);
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  if (!parse(argc, argv, a)) return usage();
+  if (a.cmd == "spawn") return do_spawn(a);
+  if (a.cmd == "interrupt") return do_signal(a, SIGINT);
+  if (a.cmd == "terminate") return do_signal(a, SIGTERM);
+  if (a.cmd == "kill") return do_signal(a, SIGKILL);
+  if (a.cmd == "ls") return do_ls(a);
+  if (a.cmd == "status") return do_status(a);
+  if (a.cmd == "wait") return do_wait(a);
+  return usage();
+}

@@ -1,0 +1,128 @@
+// th-probe: low-duty-cycle device probe for MI355X contention telemetry.
+//
+// One 256-thread workgroup per XCD-slot (grid = 8 by default; the XCD each workgroup actually
+// landed on is read from HW_REG_XCC_ID, placement is never assumed).  Each workgroup times
+//   (1) a short chain of v_mfma_f32_32x32x16_bf16 on every wave (matrix-pipe availability), and
+//   (2) a short non-temporal streaming read of its own HBM slice (memory-path availability)
+// with s_memrealtime (100 MHz constant clock, immune to DVFS).  Per-wave timings are reduced
+// through LDS (max over waves = the workgroup's phase time) and written to pinned host memory.
+// The host compares against an idle-device baseline: mfma_busy ~ 1 - t_idle/t_now and
+// hbm_bw_share ~ 1 - bw_now/bw_idle.  A probe costs tens of microseconds; at one probe per
+// second the device-time budget is < 0.01 %.
+#include "th_common.h"
+
+typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
+typedef float f32x16_p __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void th_probe_kernel(const float4v* __restrict__ hbm, long per_wg_vec,
+                                                      int mfma_iters, unsigned long long* __restrict__ out,
+                                                      float* __restrict__ sink) {
+  __shared__ unsigned long long red[4][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  bf16x8_p a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)(0.001f * (lane + j));
+    b[j] = (__bf16)(0.002f * (lane - j));
+  }
+  f32x16_p acc0 = f32x16_p(0.f), acc1 = f32x16_p(0.f);
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < mfma_iters; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, acc1, 0, 0, 0);
+  }
+  asm volatile("s_nop 15" ::: "memory");
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  const float4v* src = hbm + (long)blockIdx.x * per_wg_vec;
+  float4v s = float4v(0.f);
+  for (long i = threadIdx.x; i < per_wg_vec; i += blockDim.x) s += __builtin_nontemporal_load(src + i);
+  float part = s[0] + s[1] + s[2] + s[3];
+  part = wave_sum(part);
+  const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    red[w][0] = t1 - t0;
+    red[w][1] = t2 - t1;
+  }
+  // keep the MFMA chain and the loads alive
+  if (acc0[0] + acc1[0] + part == 1234567.0f) sink[0] = acc0[1] + acc1[1] + part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0, h = 0;
+    for (int i = 0; i < 4; ++i) {
+      m = red[i][0] > m ? red[i][0] : m;
+      h = red[i][1] > h ? red[i][1] : h;
+    }
+    unsigned long long* o = out + 4 * blockIdx.x;
+    o[0] = xcc_id();
+    o[1] = m;
+    o[2] = h;
+    o[3] = (unsigned long long)per_wg_vec * 16ull;
+  }
+}
+
+namespace {
+struct ProbeState {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  float4v* hbm = nullptr;
+  float* sink = nullptr;
+  unsigned long long* host = nullptr;  // pinned, device-mapped
+  int max_wg = 0;
+  long per_wg_vec = 0;
+};
+ProbeState g_probe;
+}  // namespace
+
+// Allocate the probe's buffers on `device`: `slice_kb` KB of HBM per workgroup, up to `max_wg`.
+extern "C" int th_probe_init(int device, int max_wg, int slice_kb) {
+  if (g_probe.device >= 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) return 1;
+  g_probe.max_wg = max_wg;
+  g_probe.per_wg_vec = (long)slice_kb * 1024 / 16;
+  if (hipStreamCreateWithFlags(&g_probe.stream, hipStreamNonBlocking) != hipSuccess) return 2;
+  if (hipMalloc((void**)&g_probe.hbm, (size_t)max_wg * g_probe.per_wg_vec * 16) != hipSuccess) return 3;
+  hipMemsetAsync(g_probe.hbm, 0, (size_t)max_wg * g_probe.per_wg_vec * 16, g_probe.stream);
+  if (hipMalloc((void**)&g_probe.sink, 64) != hipSuccess) return 4;
+  if (hipHostMalloc((void**)&g_probe.host, (size_t)max_wg * 4 * 8, hipHostMallocMapped) != hipSuccess) return 5;
+  hipStreamSynchronize(g_probe.stream);
+  g_probe.device = device;
+  return 0;
+}
+
+// Run one probe; out[5*i..] = {xcc_id, mfma_us, hbm_us, hbm_GBps, bytes} for workgroup i.
+extern "C" int th_probe_sample(int n_wg, int mfma_iters, double* out) {
+  if (g_probe.device < 0 || n_wg <= 0 || n_wg > g_probe.max_wg) return -1;
+  unsigned long long* dev_host = nullptr;
+  if (hipHostGetDevicePointer((void**)&dev_host, g_probe.host, 0) != hipSuccess) return 2;
+  th_probe_kernel<<<n_wg, 256, 0, g_probe.stream>>>(g_probe.hbm, g_probe.per_wg_vec, mfma_iters, dev_host,
+                                                    g_probe.sink);
+  if (hipGetLastError() != hipSuccess) return 3;
+  if (hipStreamSynchronize(g_probe.stream) != hipSuccess) return 4;
+  for (int i = 0; i < n_wg; ++i) {
+    const unsigned long long* r = g_probe.host + 4 * i;
+    const double mfma_us = r[1] / 100.0, hbm_us = r[2] / 100.0;  // 100 MHz ticks
+    out[5 * i + 0] = (double)r[0];
+    out[5 * i + 1] = mfma_us;
+    out[5 * i + 2] = hbm_us;
+    out[5 * i + 3] = hbm_us > 0 ? (double)r[3] / (hbm_us * 1e-6) / 1e9 : 0.0;
+    out[5 * i + 4] = (double)r[3];
+  }
+  return n_wg;
+}
+
+extern "C" int th_probe_shutdown(void) {
+  if (g_probe.device < 0) return 0;
+  hipFree(g_probe.hbm);
+  hipFree(g_probe.sink);
+  hipHostFree(g_probe.host);
+  hipStreamDestroy(g_probe.stream);
+  g_probe = ProbeState();
+  return 0;
+}
