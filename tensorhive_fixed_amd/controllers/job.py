@@ -1,0 +1,249 @@
+"""Jobs: CRUD, execute/stop, enqueue/dequeue, task membership (reference ``controllers/job.py``).
+
+``business_execute`` spawns every task of the job in PARALLEL (one thread per task; the
+reference spawned serially, 2 SSH round trips per task) and wakes the scheduler on queue
+changes so a queued job starts in well under a second when GPUs are free.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import logging
+
+from ..models.orm import Job, JobStatus, Task
+from ..utils.exceptions import ForbiddenException
+from . import task as task_ctl
+from ._common import Abort, M, check_fields, guarded, is_admin, me, snake
+
+log = logging.getLogger(__name__)
+
+
+def _owned(id: int, admin_ok: bool = True) -> Job:
+    job = Job.get(id)
+    if not ((admin_ok and is_admin()) or job.user_id == me()):
+        raise Abort(403, M("general.unprivileged"))
+    return job
+
+
+@guarded(not_found="job.not_found")
+def get_by_id(id: int):
+    job = _owned(id)
+    return {"msg": M("job.get.success"), "job": job.as_dict()}, 200
+
+
+@guarded(not_found="job.not_found", forbidden="job.all.forbidden")
+def get_all(userId: int | None = None):
+    if userId:
+        if not (is_admin() or me() == userId):
+            raise ForbiddenException("not an owner")
+        jobs = Job.query.filter(Job.user_id == userId).all()
+    else:
+        if not is_admin():
+            raise ForbiddenException("unauthorized")
+        jobs = Job.all()
+    cache = task_ctl.SessionCache()
+    for j in jobs:
+        for t in j.tasks:
+            task_ctl.synchronize(t.id, cache)
+    return {"msg": M("job.all.success"), "jobs": [j.as_dict() for j in jobs]}, 200
+
+
+@guarded(assertion="job.create.failure.invalid")
+def create(job: dict):
+    if job["userId"] != me():
+        raise Abort(403, M("general.unprivileged"))
+    try:
+        j = Job(name=job["name"], description=job.get("description"), user_id=job["userId"],
+                start_at=job.get("startAt"), stop_at=job.get("stopAt"))
+    except ValueError:
+        return {"msg": M("job.create.failure.invalid", reason="invalid date format")}, 422
+    j.save()
+    _wake("job")
+    return {"msg": M("job.create.success"), "job": j.as_dict()}, 201
+
+
+@guarded(not_found="job.not_found", forbidden="job.update.failure.forbidden",
+         assertion="job.update.failure.assertions")
+def update(id: int, newValues: dict):
+    job = Job.get(id)
+    if not (is_admin() or job.user_id == me()):
+        raise ForbiddenException("not an owner")
+    check_fields(newValues, {"name", "description", "startAt", "stopAt"})
+    assert job.status is not JobStatus.running, "must be stopped first"
+    for k, v in newValues.items():
+        if v is not None:
+            setattr(job, snake(k), v)
+    job.save()
+    _wake("job")
+    return {"msg": M("job.update.success"), "job": job.as_dict()}, 200
+
+
+@guarded(not_found="job.not_found", forbidden="job.update.failure.forbidden",
+         assertion="job.delete.failure.assertions")
+def delete(id: int):
+    job = Job.get(id)
+    if not (is_admin() or job.user_id == me()):
+        raise ForbiddenException("not an owner")
+    assert job.status is not JobStatus.running, "must be stopped first"
+    job.destroy()
+    return {"msg": M("job.delete.success")}, 200
+
+
+def _job_and_task(job_id: int, task_id: int):
+    from sqlalchemy.exc import NoResultFound
+
+    try:
+        job = Job.get(job_id)
+    except NoResultFound:
+        raise Abort(404, M("job.not_found"))
+    try:
+        task = Task.get(task_id)
+    except NoResultFound:
+        raise Abort(404, M("task.not_found"))
+    if job.user_id != me():
+        raise Abort(403, M("job.tasks.add.failure.assertions", reason="Not an owner"))
+    return job, task
+
+
+@guarded(invalid="job.tasks.add.failure.duplicate", assertion="job.tasks.add.failure.assertions",
+         assertion_status=403)
+def add_task(job_id: int, task_id: int):
+    job, task = _job_and_task(job_id, task_id)
+    job.add_task(task)
+    return {"msg": M("job.tasks.add.success"), "job": job.as_dict()}, 200
+
+
+@guarded(invalid="job.tasks.remove.failure.not_found", invalid_status=404,
+         assertion="job.tasks.remove.failure.assertions", assertion_status=403)
+def remove_task(job_id: int, task_id: int):
+    job, task = _job_and_task(job_id, task_id)
+    job.remove_task(task)
+    return {"msg": M("job.tasks.remove.success"), "job": job.as_dict()}, 200
+
+
+@guarded(not_found="job.not_found")
+def execute(id: int):
+    job = Job.get(id)
+    if job.user_id != me():
+        raise Abort(403, M("general.unprivileged"))
+    return business_execute(id)
+
+
+def _fan_out(fn, items):
+    """Run blocking node operations (spawn/terminate over the transports) concurrently; the DB
+    work around them stays on the calling thread."""
+    if len(items) <= 1:
+        return [fn(*it) for it in items]
+    with cf.ThreadPoolExecutor(max_workers=min(16, len(items))) as ex:
+        return list(ex.map(lambda it: fn(*it), items))
+
+
+@guarded(not_found="job.not_found")
+def business_execute(id: int):
+    from ..core import task_nursery
+    from ..models.orm import TaskStatus
+
+    job = Job.get(id)
+    if job.status is JobStatus.running:
+        return {"msg": M("job.execute.failure.state", reason="Job is already running")}, 409
+    cache = task_ctl.SessionCache()
+    failed, todo = [], []
+    for t in job.tasks:
+        task_ctl.synchronize(t.id, cache)
+        if t.status is TaskStatus.running or not t.full_command or not t.hostname or job.user is None:
+            failed.append(t.id)
+            continue
+        todo.append((t, (t.full_command, t.hostname, job.user.username, str(t.id))))
+
+    def spawn(cmd, host, user, tid):
+        try:
+            return task_nursery.spawn(cmd, host, user, name_appendix=tid)
+        except Exception as e:  # noqa: BLE001
+            log.warning("spawn of task %s failed: %s", tid, e)
+            return None
+
+    pids = _fan_out(spawn, [args for _t, args in todo])
+    for (t, _args), pid in zip(todo, pids):
+        if pid is None:
+            failed.append(t.id)
+            continue
+        t.pid = pid
+        t.status = TaskStatus.running
+        t.save()
+    job.synchronize_status()
+    job.save()
+    if failed:
+        return {"msg": M("job.execute.failure.tasks", reason="Could not spawn some tasks"),
+                "not_spawned_list": failed}, 422
+    return {"msg": M("job.execute.success"), "job": job.as_dict()}, 200
+
+
+@guarded(not_found="job.not_found", assertion="job.enqueue.failure", assertion_status=409)
+def enqueue(id: int):
+    job = _owned(id)
+    job.enqueue()
+    _wake("enqueue")
+    return {"msg": M("job.enqueue.success"), "job": job.as_dict()}, 200
+
+
+@guarded(not_found="job.not_found", assertion="job.dequeue.failure", assertion_status=409)
+def dequeue(id: int):
+    job = _owned(id)
+    job.dequeue()
+    return {"msg": M("job.dequeue.success"), "job": job.as_dict()}, 200
+
+
+@guarded(not_found="job.not_found")
+def stop(id: int, gracefully: bool | None = True):
+    job = Job.get(id)
+    if not (me() == job.user_id or is_admin()):
+        raise Abort(403, M("general.unprivileged"))
+    if job.status is not JobStatus.running:
+        return {"msg": M("job.stop.failure.state", reason="Only running jobs can be stopped")}, 409
+    return business_stop(id, gracefully)
+
+
+@guarded(not_found="job.not_found")
+def business_stop(id: int, gracefully: bool | None = True):
+    from ..core import task_nursery
+    from ..models.orm import TaskStatus
+
+    job = Job.get(id)
+    cache = task_ctl.SessionCache()
+    bad, todo = 0, []
+    for t in job.tasks:
+        task_ctl.synchronize(t.id, cache)
+        if t.status is not TaskStatus.running or not t.pid:
+            continue
+        todo.append((t.pid, t.hostname, job.user.username))
+
+    def term(pid, host, user):
+        try:
+            return task_nursery.terminate(pid, host, user, gracefully=gracefully)
+        except Exception as e:  # noqa: BLE001
+            log.warning("terminate of pid %s on %s failed: %s", pid, host, e)
+            return -1
+
+    bad = sum(1 for code in _fan_out(term, todo) if code != 0)
+    if bad:
+        return {"msg": M("job.stop.failure.tasks", reason="Not all tasks could be terminated")}, 422
+    if job.start_at:
+        job.start_at = None  # a manually stopped job is not auto-started again
+    job.synchronize_status()
+    job.save()
+    _wake("stop")
+    return {"msg": M("job.stop.success"), "job": job.as_dict()}, 200
+
+
+def get_templates():
+    """Launch templates for the task creator (PyTorch-ROCm torchrun, TF_CONFIG, ClusterSpec)."""
+    from ..core.launcher import TEMPLATES
+
+    return {"msg": M("general.success"), "templates": TEMPLATES}, 200
+
+
+def _wake(reason: str) -> None:
+    from ..api.app import daemon
+
+    d = daemon()
+    if d is not None:
+        d.wake(reason)

@@ -1,0 +1,154 @@
+"""Monitoring endpoints ``/nodes/*`` (reference ``controllers/nodes.py``).
+
+Served straight from the daemon's current immutable telemetry snapshot: no SSH, no lock.
+Every read auto-registers newly seen GPUs as ``Resource`` rows (as the reference does) but only
+when the snapshot version changed since the last registration (the reference inserted on every
+read path).  Non-admins see only GPUs their restrictions allow.  Responses carry the sample age
+(``X-Sample-Age-Ms`` header / ``sampleAgeMs`` in topology) so dashboards can show staleness.
+"""
+from __future__ import annotations
+
+import copy
+import threading
+
+from flask import Response
+
+from ..api.app import daemon
+from ..database import db_session
+from ..models.orm import Resource, User
+from ._common import M, is_admin, me
+
+_reg_lock = threading.Lock()
+
+
+def _snapshot():
+    d = daemon()
+    if d is None:
+        return None
+    return d.infrastructure.snapshot()
+
+
+def register_resources_from_snapshot(snap=None) -> None:
+    snap = snap or _snapshot()
+    d = daemon()
+    if snap is None or d is None:
+        return
+    with _reg_lock:
+        _registered_version = d.__dict__.setdefault("_resource_registration", {"v": -1, "ids": set()})
+        if snap.version == _registered_version["v"]:
+            return
+        known = _registered_version["ids"]
+        new = []
+        for host, entry in snap.data.items():
+            for uuid, g in ((entry or {}).get("GPU") or {}).items():
+                if uuid not in known:
+                    new.append((uuid, g.get("name"), host))
+        if new:
+            existing = {r.id for r in Resource.query.filter(Resource.id.in_([u for u, _, _ in new])).all()}
+            for uuid, name, host in new:
+                if uuid not in existing:
+                    db_session.add(Resource(id=uuid, name=(name or "")[:40], hostname=host))
+                known.add(uuid)
+            db_session.commit()
+        _registered_version["v"] = snap.version
+
+
+def get_infrastructure() -> dict:
+    snap = _snapshot()
+    if snap is None:
+        return {}
+    register_resources_from_snapshot(snap)
+    infra = copy.deepcopy(snap.data)
+    if not is_admin():
+        user = User.get(me())
+        infra = user.filter_infrastructure_by_user_restrictions(infra)
+    return infra
+
+
+def _with_age(content, status=200):
+    import json
+    import time
+
+    snap = _snapshot()
+    resp = Response(json.dumps(content, default=str), status=status, mimetype="application/json")
+    if snap is not None and snap.sampled_at:
+        resp.headers["X-Sample-Age-Ms"] = str(int(1000 * (time.time() - min(snap.sampled_at.values()))))
+    return resp
+
+
+def get_all_data():
+    return _with_age(get_infrastructure())
+
+
+def get_hostnames():
+    return list(get_infrastructure().keys()), 200
+
+
+def _host(hostname: str):
+    infra = get_infrastructure()
+    if hostname not in infra:
+        return None
+    return infra[hostname]
+
+
+def _not_found():
+    return {"msg": M("nodes.hostname.not_found")}, 404
+
+
+def get_gpu_info(hostname: str):
+    h = _host(hostname)
+    if h is None:
+        return _not_found()
+    gpus = h.get("GPU") or {}
+    return {u: {"name": g.get("name"), "index": g.get("index"), "bdf": g.get("bdf"),
+                "numa_node": g.get("numa_node")} for u, g in gpus.items()}, 200
+
+
+def get_gpu_metrics(hostname: str, metric_type: str | None = None):
+    h = _host(hostname)
+    if h is None:
+        return _not_found()
+    gpus = h.get("GPU") or {}
+    if metric_type is None:
+        return _with_age({u: g.get("metrics") for u, g in gpus.items()})
+    return _with_age({u: (g.get("metrics") or {}).get(metric_type, {"value": None, "unit": None})
+                      for u, g in gpus.items()})
+
+
+def get_cpu_metrics(hostname: str, metric_type: str | None = None):
+    h = _host(hostname)
+    if h is None:
+        return _not_found()
+    cpus = h.get("CPU") or {}
+    if metric_type is None:
+        return {k: c.get("metrics") for k, c in cpus.items()}, 200
+    return {k: (c.get("metrics") or {}).get(metric_type, {"value": None, "unit": None}) for k, c in cpus.items()}, 200
+
+
+def get_gpu_processes(hostname: str):
+    h = _host(hostname)
+    if h is None:
+        return _not_found()
+    gpus = h.get("GPU") or {}
+    return {u: g.get("processes") for u, g in gpus.items()}, 200
+
+
+def get_topology():
+    """xGMI link matrix + NUMA + BDF per host (new; feeds rank->device placement)."""
+    d = daemon()
+    if d is None:
+        return {}, 200
+    return d.topology(), 200
+
+
+def get_internal_metrics():
+    """Service loop timings and API latency percentiles (observability, new)."""
+    from flask import current_app
+
+    d = daemon()
+    out = {"api": current_app.extensions["tensorhive_fixed_amd"]["latency"].summary()}
+    if d is not None:
+        out["services"] = d.service_stats()
+        snap = d.infrastructure.snapshot()
+        out["snapshot_version"] = snap.version
+    return out, 200

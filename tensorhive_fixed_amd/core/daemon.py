@@ -1,0 +1,146 @@
+"""The daemon object (reference ``core/managers/{TensorHiveManager,ServiceManager}.py``).
+
+Explicit dependency injection instead of a metaclass singleton: one :class:`Daemon` owns the
+config, infrastructure store, transports, telemetry backends and services; the Flask app gets
+it through ``create_app(daemon)``.  Startup mirrors ``TensorHiveManager.__init__``: load/create
+the dedicated SSH key, refuse an empty hosts config, optionally test SSH, then build services.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+
+from ..config import Config, get_config
+from ..utils.exceptions import ConfigurationException
+from .infrastructure import InfrastructureStore
+from .services import (JobSchedulingService, MonitoringService, ProtectionService, Service,
+                       UsageLoggingService)
+from .telemetry import StubBackend, TelemetryBackend, make_backend
+from .transport import TransportManager
+
+log = logging.getLogger(__name__)
+
+
+class Daemon:
+    def __init__(self, cfg: Config | None = None, transports: TransportManager | None = None,
+                 backends: dict[str, TelemetryBackend] | None = None, init_key: bool = True,
+                 test_ssh: bool | None = None):
+        self.cfg = cfg or get_config()
+        nodes = self.cfg.ssh.available_nodes
+        if not nodes:
+            raise ConfigurationException(
+                f"no hosts configured in {self.cfg.ssh.hosts_config_file}; add at least one [hostname] section")
+        self.ssh_key_path = self.cfg.ssh.key_file
+        if init_key:
+            from . import ssh
+
+            try:
+                ssh.init_ssh_key(self.ssh_key_path)
+            except Exception as e:  # noqa: BLE001 -- ssh-keygen missing etc.
+                log.warning("could not create the dedicated SSH key: %s", e)
+        self.transports = transports or TransportManager.from_config(nodes, self.ssh_key_path, self.cfg.ssh.proxy,
+                                                                    self.cfg.ssh.timeout)
+        if test_ssh if test_ssh is not None else self.cfg.ssh.test_on_startup:
+            bad = [h for h, ok in self.transports.test_all(self.cfg.ssh.timeout).items() if not ok]
+            if bad:
+                log.warning("SSH test failed for: %s", ", ".join(bad))
+        self.infrastructure = InfrastructureStore(list(nodes))
+        if backends is None:
+            am = self.cfg.amd_monitor
+            shared: dict = {}
+            backends = {}
+            for h in nodes:
+                kind = am.backend
+                b = make_backend(kind, h, self.transports, am.stub_gpus, am.probe_enabled, am.probe_period,
+                                 stream_ms=int(1000 * self.cfg.monitoring.update_interval))
+                # one StubBackend / AmdSmiBackend instance is enough for all hosts of that kind
+                backends[h] = shared.setdefault(type(b).__name__, b) if isinstance(b, StubBackend) else b
+        self.backends = backends
+        self.services: list[Service] = []
+        self._topology_cache: dict = {}
+        self._lock = threading.Lock()
+
+    # ------------------------------------------------------------------ services
+    def configure_services_from_config(self) -> list[Service]:
+        from .violation_handlers import (EmailSendingBehaviour, MessageSendingBehaviour, ProtectionHandler,
+                                         SudoProcessKillingBehaviour, UserProcessKillingBehaviour)
+
+        c = self.cfg
+        svcs: list[Service] = []
+        if c.monitoring.enabled:
+            svcs.append(MonitoringService(c.monitoring.update_interval, self.backends if c.monitoring.enable_gpu_monitor
+                                          else {h: StubBackend(0) for h in self.backends}))
+        if c.protection.level > 0:
+            handlers = []
+            if c.protection.notify_on_pty:
+                handlers.append(ProtectionHandler(MessageSendingBehaviour(self.transports)))
+            if c.protection.notify_via_email:
+                handlers.append(ProtectionHandler(EmailSendingBehaviour(c.mailbot)))
+            if c.protection.kill_processes == 1:
+                handlers.append(ProtectionHandler(UserProcessKillingBehaviour(self.transports)))
+            elif c.protection.kill_processes == 2:
+                handlers.append(ProtectionHandler(SudoProcessKillingBehaviour(self.transports)))
+            svcs.append(ProtectionService(c.protection.update_interval, handlers, c.protection.level))
+        if c.usage_logging.enabled:
+            svcs.append(UsageLoggingService(c.usage_logging.update_interval, c.usage_logging.log_dir,
+                                            c.usage_logging.log_cleanup_action))
+        if c.job_scheduling.enabled:
+            svcs.append(JobSchedulingService(c.job_scheduling.update_interval,
+                                             c.job_scheduling.stop_termination_attempts_after_mins,
+                                             c.job_scheduling.schedule_queued_jobs_when_free_mins))
+        for s in svcs:
+            s.inject(self)
+        self.services = svcs
+        return svcs
+
+    def add_service(self, svc: Service) -> None:
+        svc.inject(self)
+        self.services.append(svc)
+
+    def service(self, cls):
+        for s in self.services:
+            if isinstance(s, cls):
+                return s
+        return None
+
+    def init(self) -> None:
+        for s in self.services:
+            s.start()
+
+    start = init
+
+    def shutdown(self, timeout: float = 5.0) -> None:
+        for s in self.services:
+            s.stop()
+        for s in self.services:
+            if s.is_alive():
+                s.join(timeout)
+        for b in set(map(id, self.backends.values())):
+            pass
+        for b in {id(b): b for b in self.backends.values()}.values():
+            try:
+                b.close()
+            except Exception:  # noqa: BLE001
+                pass
+        self.transports.close()
+
+    def wake(self, reason: str = "") -> None:
+        """Event-driven wake-up of the job scheduler (enqueue, reservation change, job stop)."""
+        s = self.service(JobSchedulingService)
+        if s is not None:
+            s.wake()
+
+    # ------------------------------------------------------------------ introspection
+    def topology(self) -> dict:
+        out = {}
+        for h, b in self.backends.items():
+            if h not in self._topology_cache:
+                try:
+                    self._topology_cache[h] = b.topology(h)
+                except Exception as e:  # noqa: BLE001
+                    self._topology_cache[h] = {"error": str(e)}
+            out[h] = self._topology_cache[h]
+        return out
+
+    def service_stats(self) -> dict:
+        return {s.name: {"ticks": s.ticks, "interval_s": s.interval, **s.stats.summary()} for s in self.services}

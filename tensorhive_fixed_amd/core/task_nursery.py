@@ -1,0 +1,132 @@
+"""Remote task lifecycle on top of the native ``th-run`` supervisor (reference
+``core/task_nursery.py:1-315``, which drove GNU ``screen`` over SSH).
+
+Public functions keep the reference's shape:
+  * :func:`spawn` -> pid of the task's process group leader (the command itself, not a screen
+    wrapper, so GPU process lists and task PIDs can be matched);
+  * :func:`terminate` -- ``gracefully=True`` SIGINT, ``None`` SIGTERM (was ``screen -X quit``),
+    ``False`` SIGKILL, always to the whole process group (torchrun + every rank);
+  * :func:`running` -- live sessions of a user on a host, ONE round trip per host (``th-run ls``);
+  * :func:`fetch_log` -- ``~/TensorHiveLogs/task_<id>.log`` (whole file or tail).
+Names (``tensorhive_task_<id>``) and log paths are unchanged.  Every task gets
+``TENSORHIVE_TASK_ID=<id>`` in its environment, which the telemetry uses to attribute GPU
+processes to tasks exactly.  If ``th-run`` is not installed on a remote node, a ``setsid`` +
+``tee`` shell fallback keeps spawn/kill/log working.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import shlex
+
+from ..config import get_config
+from . import ssh
+from .transport import Result, TransportManager
+
+log = logging.getLogger(__name__)
+
+SESSION_PREFIX = "tensorhive_task_"
+
+
+class SpawnError(Exception):
+    pass
+
+
+class ExitCodeError(Exception):
+    pass
+
+
+def session_name(task_id) -> str:
+    return f"{SESSION_PREFIX}{task_id}"
+
+
+def log_path(task_id) -> str:
+    d = get_config().launcher.log_dir.rstrip("/")
+    return f"{d}/task_{task_id}.log"
+
+
+def _th_run(host: str) -> str:
+    spec = get_config().ssh.available_nodes.get(host, {})
+    if spec.get("transport") == "local":
+        from ..native.build import th_run_binary
+
+        return th_run_binary()
+    return get_config().launcher.supervisor
+
+
+def _client(host: str, user: str) -> TransportManager:
+    return ssh.get_client(*ssh.build_dedicated_config_for(host, user))
+
+
+def _run(host: str, user: str, cmd: str, timeout: float | None = None) -> Result:
+    return _client(host, user).run(host, cmd, timeout=timeout or get_config().ssh.timeout + 20)
+
+
+def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | None = None) -> str:
+    name = session_name(task_id)
+    logf = log_path(task_id)
+    env = {"TENSORHIVE_TASK_ID": str(task_id), **(extra_env or {})}
+    env_args = " ".join(f"--env {shlex.quote(f'{k}={v}')}" for k, v in env.items())
+    th = shlex.quote(th_run)
+    primary = (f"{th} spawn --name {name} --log {logf} {env_args} -- bash -lc {shlex.quote(command)}")
+    envs = " ".join(f"{k}={shlex.quote(str(v))}" for k, v in env.items())
+    fallback = (f"mkdir -p $(dirname {logf}) && ( {envs} setsid bash -lc {shlex.quote(command)} "
+                f"> >(tee -a {logf} >/dev/null) 2>&1 < /dev/null & echo $! )")
+    return f"if command -v {th} >/dev/null 2>&1 || [ -x {th} ]; then {primary}; else {fallback}; fi"
+
+
+def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra_env: dict | None = None) -> int:
+    r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), extra_env))
+    if r.exception is not None:
+        raise SpawnError(f"connection failed: {r.exception}")
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        raise SpawnError(f"unable to parse pid from {r.stdout!r} / {r.stderr.strip()!r}")
+
+
+def terminate(pid: int, hostname: str, user: str, gracefully: bool | None = True) -> int:
+    verb = {True: "interrupt", None: "terminate", False: "kill"}[gracefully]
+    sig = {True: "INT", None: "TERM", False: "KILL"}[gracefully]
+    th = shlex.quote(_th_run(hostname))
+    cmd = (f"if command -v {th} >/dev/null 2>&1 || [ -x {th} ]; then {th} {verb} --pid {int(pid)}; "
+           f"else kill -{sig} -- -{int(pid)} 2>/dev/null || kill -{sig} {int(pid)}; fi")
+    r = _run(hostname, user, cmd)
+    if r.exception is not None:
+        raise ConnectionError(str(r.exception))
+    return r.exit_code
+
+
+def running(hostname: str, user: str) -> list[dict]:
+    """Live th-run sessions of ``user`` on ``hostname`` (dicts: name, pid, pgid, started, ...)."""
+    th = shlex.quote(_th_run(hostname))
+    r = _run(hostname, user, f"if command -v {th} >/dev/null 2>&1 || [ -x {th} ]; then {th} ls; fi")
+    if r.exception is not None:
+        raise ConnectionError(str(r.exception))
+    out = []
+    for line in r.stdout.splitlines():
+        line = line.strip()
+        if not line.startswith("{"):
+            continue
+        try:
+            d = json.loads(line)
+        except json.JSONDecodeError:
+            continue
+        if str(d.get("name", "")).startswith(SESSION_PREFIX):
+            out.append(d)
+    return out
+
+
+def running_pids(hostname: str, user: str) -> list[int]:
+    return [int(d["pid"]) for d in running(hostname, user)]
+
+
+def fetch_log(hostname: str, user: str, task_id, tail: bool = False, tail_lines: int = 10) -> tuple[list[str], str]:
+    path = log_path(task_id)
+    cmd = f"tail -n {int(tail_lines)} {path}" if tail else f"cat {path}"
+    r = _run(hostname, user, cmd)
+    if r.exception is not None:
+        raise ConnectionError(str(r.exception))
+    if r.exit_code != 0:
+        raise FileNotFoundError(path)
+    return r.stdout.splitlines(), path

@@ -1,0 +1,216 @@
+"""Node transports: how the daemon runs commands on a node (replaces parallel-ssh/libssh2).
+
+Reference: ``core/managers/SSHConnectionManager.py`` (one ParallelSSHClient over all hosts +
+cached per-host clients, optional proxy jump) and ``core/ssh.py`` (``run_command`` with
+``stop_on_errors=False``).  Here:
+
+* :class:`LocalTransport` -- fork/exec on the node the daemon runs on (no sshd needed); can run
+  as another UNIX user through ``runuser`` when the daemon is root.
+* :class:`SSHTransport` -- the OpenSSH client with **ControlMaster multiplexing** (one TCP/SSH
+  session per host and user, reused by every command: no per-command handshake), optional
+  ProxyJump, BatchMode, TensorHive's dedicated key.
+* :class:`FakeTransport` -- scripted replies + fault injection (drop host, hang, fail) for tests.
+* :class:`TransportManager` -- per-host transports from ``hosts_config.ini`` and a thread-pool
+  fan-out (``run_all``) whose per-host failures never abort the others.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import getpass
+import logging
+import os
+import re
+import shlex
+import subprocess
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Callable
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class Result:
+    host: str
+    stdout: str
+    stderr: str
+    exit_code: int
+    exception: BaseException | None = None
+
+    @property
+    def ok(self) -> bool:
+        return self.exception is None and self.exit_code == 0
+
+    @property
+    def lines(self) -> list[str]:
+        return self.stdout.splitlines()
+
+
+class Transport:
+    host: str = "localhost"
+    user: str | None = None
+
+    def run(self, command: str, timeout: float | None = None, user: str | None = None,
+            env: dict | None = None) -> Result:
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class LocalTransport(Transport):
+    def __init__(self, host: str = "localhost", user: str | None = None):
+        self.host = host
+        self.user = user
+
+    def _argv(self, command: str, user: str | None) -> list[str]:
+        me = getpass.getuser()
+        if user and user != me:
+            if os.geteuid() == 0:
+                return ["runuser", "-u", user, "--", "bash", "-lc", command]
+            log.debug("local transport cannot switch to %s (not root); running as %s", user, me)
+        return ["bash", "-c", command]
+
+    def run(self, command, timeout=None, user=None, env=None) -> Result:
+        try:
+            p = subprocess.run(self._argv(command, user or self.user), capture_output=True, text=True,
+                               timeout=timeout, env={**os.environ, **(env or {})})
+            return Result(self.host, p.stdout, p.stderr, p.returncode)
+        except subprocess.TimeoutExpired as e:
+            return Result(self.host, e.stdout or "", e.stderr or "", 124, e)
+        except OSError as e:
+            return Result(self.host, "", str(e), 127, e)
+
+
+class SSHTransport(Transport):
+    """OpenSSH with a persistent ControlMaster per (host, user)."""
+
+    def __init__(self, host: str, user: str, port: int = 22, key_file: str | None = None,
+                 proxy: dict | None = None, timeout: float = 10.0, control_dir: str | None = None):
+        self.host, self.user, self.port = host, user, port
+        self.key_file, self.proxy, self.timeout = key_file, proxy, timeout
+        self.control_dir = Path(control_dir or os.path.expanduser("~/.cache/tensorhive/ssh"))
+        self.control_dir.mkdir(parents=True, exist_ok=True, mode=0o700)
+
+    def base_argv(self, user: str | None = None) -> list[str]:
+        u = user or self.user
+        argv = ["ssh", "-p", str(self.port), "-o", "BatchMode=yes", "-o", "StrictHostKeyChecking=accept-new",
+                "-o", f"ConnectTimeout={int(max(1, self.timeout))}", "-o", "ControlMaster=auto",
+                "-o", f"ControlPath={self.control_dir}/%r@%h:%p", "-o", "ControlPersist=600",
+                "-o", "ServerAliveInterval=15"]
+        if self.key_file:
+            argv += ["-i", self.key_file, "-o", "IdentitiesOnly=yes"]
+        if self.proxy:
+            argv += ["-J", f"{self.proxy['proxy_user']}@{self.proxy['proxy_host']}:{self.proxy.get('proxy_port', 22)}"]
+        return argv + [f"{u}@{self.host}"]
+
+    def run(self, command, timeout=None, user=None, env=None) -> Result:
+        if env:
+            command = " ".join(f"{k}={shlex.quote(str(v))}" for k, v in env.items()) + " " + command
+        argv = self.base_argv(user) + [command]
+        try:
+            p = subprocess.run(argv, capture_output=True, text=True, timeout=timeout or (self.timeout + 60))
+            exc = None
+            if p.returncode == 255:  # ssh itself failed (connection/auth)
+                exc = ConnectionError(p.stderr.strip() or "ssh connection failed")
+            return Result(self.host, p.stdout, p.stderr, p.returncode, exc)
+        except subprocess.TimeoutExpired as e:
+            return Result(self.host, "", "timeout", 124, e)
+        except OSError as e:
+            return Result(self.host, "", str(e), 127, e)
+
+    def close(self) -> None:
+        subprocess.run(self.base_argv()[:-1] + ["-O", "exit", f"{self.user}@{self.host}"], capture_output=True)
+
+
+class FakeTransport(Transport):
+    """Scripted transport for tests: ``rules`` are (regex, handler|Result-like tuple)."""
+
+    def __init__(self, host: str, user: str = "tensorhive"):
+        self.host, self.user = host, user
+        self.rules: list[tuple[re.Pattern, Callable[[str, str | None], tuple[str, str, int]]]] = []
+        self.calls: list[tuple[str, str | None]] = []
+        self.down = False
+        self.hang = 0.0
+        self._lock = threading.Lock()
+
+    def on(self, pattern: str, reply) -> "FakeTransport":
+        fn = reply if callable(reply) else (lambda _c, _u, r=reply: r)
+        self.rules.append((re.compile(pattern), fn))
+        return self
+
+    def run(self, command, timeout=None, user=None, env=None) -> Result:
+        with self._lock:
+            self.calls.append((command, user))
+        if self.down:
+            return Result(self.host, "", "host unreachable", 255, ConnectionError("host unreachable"))
+        if self.hang:
+            time.sleep(min(self.hang, timeout or self.hang))
+            return Result(self.host, "", "timeout", 124, TimeoutError("hang"))
+        for pat, fn in self.rules:
+            if pat.search(command):
+                out, err, rc = fn(command, user)
+                return Result(self.host, out, err, rc)
+        return Result(self.host, "", f"no rule for: {command}", 127)
+
+
+@dataclass
+class TransportManager:
+    """Per-host transports + parallel fan-out (``stop_on_errors=False`` semantics)."""
+
+    transports: dict[str, Transport] = field(default_factory=dict)
+    max_workers: int = 32
+
+    @classmethod
+    def from_config(cls, nodes: dict[str, dict], key_file: str | None, proxy: dict | None,
+                    timeout: float = 10.0) -> "TransportManager":
+        tm = cls()
+        for host, spec in nodes.items():
+            kind = spec.get("transport", "ssh")
+            if kind == "local" or (kind == "auto" and host in ("localhost", "127.0.0.1")):
+                tm.transports[host] = LocalTransport(host, spec.get("user"))
+            else:
+                tm.transports[host] = SSHTransport(host, spec.get("user") or getpass.getuser(),
+                                                   int(spec.get("port", 22)), key_file, proxy, timeout)
+        return tm
+
+    def hosts(self) -> list[str]:
+        return list(self.transports)
+
+    def get(self, host: str) -> Transport:
+        t = self.transports.get(host)
+        if t is None:
+            raise KeyError(f"unknown host {host}")
+        return t
+
+    def run(self, host: str, command: str, **kw) -> Result:
+        return self.get(host).run(command, **kw)
+
+    def run_all(self, command: str | Callable[[str], str], hosts: list[str] | None = None,
+                timeout: float | None = None) -> dict[str, Result]:
+        hosts = hosts or self.hosts()
+        if not hosts:
+            return {}
+        with cf.ThreadPoolExecutor(max_workers=min(self.max_workers, len(hosts))) as ex:
+            futs = {h: ex.submit(self.transports[h].run, command(h) if callable(command) else command,
+                                 timeout=timeout) for h in hosts}
+            out = {}
+            for h, f in futs.items():
+                try:
+                    out[h] = f.result()
+                except Exception as e:  # noqa: BLE001
+                    out[h] = Result(h, "", str(e), 1, e)
+            return out
+
+    def test_all(self, timeout: float = 10.0) -> dict[str, bool]:
+        """``uname`` on every host (reference ``test_all_connections``)."""
+        return {h: r.ok for h, r in self.run_all("uname", timeout=timeout).items()}
+
+    def close(self) -> None:
+        for t in self.transports.values():
+            try:
+                t.close()
+            except Exception:  # noqa: BLE001
+                pass

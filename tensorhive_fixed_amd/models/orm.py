@@ -414,8 +414,10 @@ class Restriction(CRUDModel, Base):
     _starts_at = Column("starts_at", DateTime, nullable=False)
     _ends_at = Column("ends_at", DateTime)
     is_global = Column(Boolean, nullable=False)
-    _users = relationship("User", secondary="restriction2assignee", back_populates="_restrictions")
-    _groups = relationship("Group", secondary="restriction2assignee", back_populates="_restrictions")
+    _users = relationship("User", secondary="restriction2assignee", back_populates="_restrictions",
+                          overlaps="_groups")
+    _groups = relationship("Group", secondary="restriction2assignee", back_populates="_restrictions",
+                           overlaps="_users")
     _resources = relationship("Resource", secondary="restriction2resource", back_populates="_restrictions")
     _schedules = relationship("RestrictionSchedule", secondary="restriction2schedule", back_populates="_restrictions")
 

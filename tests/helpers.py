@@ -1,0 +1,12 @@
+"""Test helpers shared by API tests."""
+import json
+
+
+def api(client, method, path, headers=None, body=None, **q):
+    resp = getattr(client, method)("/api" + path, headers=headers or {}, data=None if body is None else json.dumps(body),
+                                   query_string=q or None)
+    try:
+        data = resp.get_json()
+    except Exception:  # noqa: BLE001
+        data = None
+    return resp.status_code, data

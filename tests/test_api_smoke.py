@@ -1,0 +1,45 @@
+"""Smoke-level API flows over the real router (login, reservations, nodes)."""
+import datetime
+
+from tests.helpers import api
+
+
+def test_login_and_users(client, new_user, new_admin, auth_headers):
+    st, body = api(client, "post", "/user/login", {"Content-Type": "application/json"},
+                   {"username": "administrantee", "password": "TEST PASSWORD"})
+    assert st == 200 and "access_token" in body and "refresh_token" in body
+    st, body = api(client, "get", "/users", auth_headers(new_user))
+    assert st == 200 and len(body) == 2 and "email" not in body[0]
+    st, body = api(client, "get", "/users", auth_headers(new_admin))
+    assert st == 200 and "email" in body[0]
+    st, _ = api(client, "get", "/users")
+    assert st == 401
+
+
+def test_nodes_metrics_and_resources(client, new_admin, auth_headers):
+    st, body = api(client, "get", "/nodes/metrics", auth_headers(new_admin))
+    assert st == 200 and set(body) == {"node-a", "node-b"}
+    gpus = body["node-a"]["GPU"]
+    assert len(gpus) == 8 and all(len(u) == 40 for u in gpus)
+    st, res = api(client, "get", "/resources", auth_headers(new_admin))
+    assert st == 200 and len(res) == 16
+    st, body = api(client, "get", "/nodes/node-a/gpu/metrics", auth_headers(new_admin), metric_type="power")
+    assert st == 200 and all(v["unit"] == "W" for v in body.values())
+    st, _ = api(client, "get", "/nodes/node-a/gpu/metrics", auth_headers(new_admin), metric_type="bogus")
+    assert st == 400
+    st, _ = api(client, "get", "/nodes/metrics", auth_headers(new_admin), unknown="1")
+    assert st == 400
+
+
+def test_reservation_flow(client, new_user, auth_headers, resource1, permissive_restriction):
+    permissive_restriction.apply_to_user(new_user)
+    start = datetime.datetime.utcnow() + datetime.timedelta(hours=1)
+    fmt = "%Y-%m-%dT%H:%M:%S.%fZ"
+    body = {"title": "t", "description": "d", "resourceId": resource1.id, "userId": new_user.id,
+            "start": start.strftime(fmt), "end": (start + datetime.timedelta(hours=2)).strftime(fmt)}
+    st, data = api(client, "post", "/reservations", auth_headers(new_user), body)
+    assert st == 201, data
+    assert data["reservation"]["userName"] == "administrantee"
+    assert data["reservation"]["start"].endswith("+00:00")
+    st, data = api(client, "post", "/reservations", auth_headers(new_user), body)
+    assert st == 422  # overlap
