@@ -256,8 +256,15 @@ def create_app(daemon_obj=None) -> Flask:
         db_session.rollback()
         return jsonify({"msg": cfg.api.responses["general"]["internal_error"]}), 500
 
+    app.config.setdefault("TH_REMOVE_SESSION", True)
+
     @app.teardown_appcontext
     def remove_session(_exc=None):
-        db_session.remove()
+        # one session per request thread; in-process test clients share the caller's thread
+        # and keep it (TH_REMOVE_SESSION=False) so fixtures stay attached
+        if app.config["TH_REMOVE_SESSION"]:
+            db_session.remove()
+        else:
+            db_session.rollback() if _exc is not None else None
 
     return app

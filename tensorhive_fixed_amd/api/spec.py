@@ -193,7 +193,7 @@ OPERATIONS: list[Op] = [
 # new, additive operations (not part of the 66 compat operations)
 EXTRA_OPERATIONS: list[Op] = [
     Op("GET", "/nodes/topology", "nodes.get_topology", "jwt", tag="nodes"),                       # new
-    Op("GET", "/metrics/internal", "nodes.get_internal_metrics", "jwt", tag="nodes"),             # new
+    Op("GET", "/metrics/internal", "nodes.get_internal_metrics", "admin", tag="nodes"),            # new
     Op("GET", "/jobs/templates", "job.get_templates", "jwt", tag="jobs"),                         # new
 ]
 

@@ -1,0 +1,222 @@
+"""Benchmark harnesses for the daemon-side metrics of BASELINE.md.
+
+* :func:`poll_latency` -- p50/p99 latency of ``GET /nodes/metrics`` (the dashboard's poll) on a
+  simulated cluster of ``nodes`` x ``gpus`` MI355X (stub telemetry, real router, real auth, real
+  snapshot path).  The reference re-read a shared dict under no lock and ran ``nvidia-smi`` per
+  node per poll interval (``core/monitors/GPUMonitor.py``); here a poll reads one RCU snapshot.
+* :func:`launch_latency` -- time from ``PUT /jobs/{id}/enqueue`` to the task's process running on
+  a local node through ``th-run`` (event-driven scheduler wake; the reference polled every 30 s,
+  ``core/services/JobSchedulingService.py:44``).
+* :func:`train_throughput` -- runs ``bench.py`` (the flagship Llama-3-8B DDP step) and returns its
+  JSON line.
+"""
+from __future__ import annotations
+
+import contextlib
+import getpass
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _pct(xs: list[float], q: float) -> float:
+    xs = sorted(xs)
+    if not xs:
+        return float("nan")
+    i = min(len(xs) - 1, max(0, int(round(q * (len(xs) - 1)))))
+    return xs[i]
+
+
+@contextlib.contextmanager
+def sandbox(hosts: dict[str, str], backend: str = "stub", stub_gpus: int = 8, job_interval: float = 30.0):
+    """Temporary config dir + file SQLite DB + installed global config.
+
+    ``hosts`` maps hostname -> transport (``local``/``fake``/``ssh``).  Restores the previous
+    config and ``TENSORHIVE_CONFIG_DIR`` on exit."""
+    from . import config as C
+    from . import database as D
+
+    old_dir = os.environ.get("TENSORHIVE_CONFIG_DIR")
+    old_state = os.environ.get("TH_RUN_STATE_DIR")
+    old_cfg = C._current
+    with tempfile.TemporaryDirectory(prefix="th-bench-") as td:
+        d = Path(td)
+        user = getpass.getuser()
+        (d / "hosts_config.ini").write_text(
+            "".join(f"[{h}]\nuser = {user}\ntransport = {t}\n\n" for h, t in hosts.items()))
+        (d / "main_config.ini").write_text(f"""
+[ssh]
+hosts_config_file = {d / 'hosts_config.ini'}
+test_on_startup = off
+key_file = {d / 'ssh_key'}
+[database]
+path = {d / 'db.sqlite'}
+[monitoring_service]
+update_interval = 1
+[protection_service]
+enabled = off
+level = 0
+[usage_logging_service]
+enabled = off
+[job_scheduling_service]
+enabled = on
+update_interval = {job_interval}
+[amd_monitor]
+backend = {backend}
+stub_gpus = {stub_gpus}
+probe_enabled = off
+[launcher]
+log_dir = {d / 'logs'}
+""")
+        C.init_config_files(d)
+        os.environ["TENSORHIVE_CONFIG_DIR"] = str(d)
+        os.environ["TH_RUN_STATE_DIR"] = str(d / "th-run")
+        cfg = C.load_config(d)
+        C.set_config(cfg)
+        D.configure(f"sqlite:///{d / 'db.sqlite'}")
+        D.create_all()
+        try:
+            yield cfg, d
+        finally:
+            D.db_session.remove()
+            for k, v in (("TENSORHIVE_CONFIG_DIR", old_dir), ("TH_RUN_STATE_DIR", old_state)):
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            C.set_config(old_cfg)
+
+
+def _admin(name: str = "bench"):
+    from .models.orm import Role, User
+
+    u = User(username=name, password="benchmark password", email=f"{name}@example.org",
+             roles=[Role(name="user"), Role(name="admin")])
+    u.save()
+    return u
+
+
+def _headers(u) -> dict:
+    from .api import auth
+
+    return {"Authorization": "Bearer " + auth.create_access_token(u.id, u.role_names, fresh=True)}
+
+
+def poll_latency(requests: int = 1000, nodes: int = 8, gpus: int = 8, warmup: int = 20) -> dict:
+    """p50/p99 of the dashboard poll on ``nodes`` x ``gpus`` simulated GPUs."""
+    from .api.app import create_app
+    from .core.daemon import Daemon
+    from .core.telemetry import StubBackend
+
+    hosts = {f"mi355x-{i:02d}": "fake" for i in range(nodes)}
+    with sandbox(hosts, stub_gpus=gpus) as (cfg, _d):
+        stub = StubBackend(gpus_per_host=gpus)
+        daemon = Daemon(cfg, backends={h: stub for h in hosts}, init_key=False, test_ssh=False)
+        for h in hosts:
+            daemon.infrastructure.publish(h, stub.sample(h))
+        client = create_app(daemon).test_client()
+        hdr = _headers(_admin())
+        out = {}
+        for path in ("/api/nodes/metrics", "/api/nodes/mi355x-00/gpu/metrics?metric_type=utilization"):
+            lat = []
+            for i in range(warmup + requests):
+                t0 = time.perf_counter()
+                r = client.get(path, headers=hdr)
+                dt = (time.perf_counter() - t0) * 1e3
+                assert r.status_code == 200, r.data[:200]
+                if i >= warmup:
+                    lat.append(dt)
+            out[path] = {"p50_ms": round(_pct(lat, 0.5), 3), "p99_ms": round(_pct(lat, 0.99), 3),
+                         "mean_ms": round(statistics.fmean(lat), 3), "requests": requests}
+        daemon.shutdown()
+        return {"metric": "dashboard_poll_latency", "nodes": nodes, "gpus_per_node": gpus, "results": out}
+
+
+def launch_latency(trials: int = 5, command: str = "sleep 2") -> dict:
+    """Enqueue -> task process running, through the real scheduler thread and th-run."""
+    from .controllers import task as task_ctl
+    from .core.daemon import Daemon
+    from .core.services import JobSchedulingService
+    from .core.telemetry import StubBackend
+    from .models.orm import (CommandSegment, Job, JobStatus, Restriction, SegmentType,
+                             Task, TaskStatus)
+    from .native.build import build_all
+    from .utils import dates
+
+    me = getpass.getuser()
+    if me == "root":
+        # tasks run as the job owner's UNIX account; "root" is not a valid TensorHive username
+        return {"metric": "queued_job_launch_latency", "skipped": "run as an ordinary user"}
+    build_all(strict=False)
+    with sandbox({"localhost": "local"}, job_interval=3600.0) as (cfg, _d):
+        stub = StubBackend(gpus_per_host=8)
+        daemon = Daemon(cfg, backends={"localhost": stub}, init_key=False, test_ssh=False)
+        daemon.infrastructure.publish("localhost", stub.sample("localhost"))
+        sched = JobSchedulingService(3600.0, 5, 10)
+        daemon.add_service(sched)
+        u = _admin(me)
+        r = Restriction(name="all", starts_at=dates.utcnow(), is_global=True)
+        r.save()
+        r.apply_to_user(u)
+        seg = CommandSegment(name="HIP_VISIBLE_DEVICES", _segment_type=SegmentType.env_variable)
+        seg.save()
+        sched.start()
+        lat = []
+        try:
+            for i in range(trials):
+                job = Job(name=f"bench-{i}", description="", user_id=u.id)
+                job.save()
+                t = Task(command=command, hostname="localhost")
+                t.save()
+                job.add_task(t)
+                t.add_cmd_segment(seg, str(i % 8))
+                job.enqueue()
+                t0 = time.time()
+                daemon.wake("enqueue")
+                deadline = time.time() + 30
+                while time.time() < deadline:
+                    if any(jid == job.id for jid, _ in sched.launch_log):
+                        break
+                    time.sleep(0.002)
+                else:
+                    raise TimeoutError(f"job {job.id} was not launched within 30 s")
+                ts = dict(sched.launch_log)[job.id]
+                lat.append((ts - t0) * 1e3)
+                from .database import db_session
+
+                db_session.expire_all()
+                t = Task.get(t.id)
+                assert t.status is TaskStatus.running and t.pid, t.as_dict()
+                from .core import task_nursery
+
+                task_nursery.terminate(t.pid, "localhost", u.username, gracefully=False)
+                task_ctl.synchronize(t.id)
+                job = Job.get(job.id)
+                job.dequeue() if job.status is JobStatus.pending else None
+        finally:
+            daemon.shutdown()
+        return {"metric": "queued_job_launch_latency", "trials": trials,
+                "p50_ms": round(_pct(lat, 0.5), 2), "max_ms": round(max(lat), 2),
+                "reference_ms": 30000.0 / 2, "note": "reference polls every 30 s -> 15 s mean wait"}
+
+
+def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3) -> dict:
+    """Run bench.py (torchrun for gpus>1) and return its JSON line."""
+    if gpus > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", "29511", str(ROOT / "bench.py"),
+               "--gpus", str(gpus), "--steps", str(steps), "--warmup", str(warmup)]
+    else:
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--steps", str(steps), "--warmup", str(warmup)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    for line in reversed(r.stdout.splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise RuntimeError(f"bench.py failed ({r.returncode}): {r.stderr[-2000:]}")

@@ -226,6 +226,9 @@ def business_stop(id: int, gracefully: bool | None = True):
     bad = sum(1 for code in _fan_out(term, todo) if code != 0)
     if bad:
         return {"msg": M("job.stop.failure.tasks", reason="Not all tasks could be terminated")}, 422
+    fresh = task_ctl.SessionCache()  # processes that already exited show up as terminated now
+    for t in job.tasks:
+        task_ctl.synchronize(t.id, fresh)
     if job.start_at:
         job.start_at = None  # a manually stopped job is not auto-started again
     job.synchronize_status()

@@ -44,6 +44,9 @@ class Daemon:
             bad = [h for h, ok in self.transports.test_all(self.cfg.ssh.timeout).items() if not ok]
             if bad:
                 log.warning("SSH test failed for: %s", ", ".join(bad))
+        from . import task_nursery
+
+        task_nursery.use_transports(self.transports)
         self.infrastructure = InfrastructureStore(list(nodes))
         if backends is None:
             am = self.cfg.amd_monitor
@@ -56,6 +59,11 @@ class Daemon:
                 # one StubBackend / AmdSmiBackend instance is enough for all hosts of that kind
                 backends[h] = shared.setdefault(type(b).__name__, b) if isinstance(b, StubBackend) else b
         self.backends = backends
+        from .transport import SimulatedNode
+
+        for h, t in self.transports.transports.items():  # simulated nodes report into the stub telemetry
+            if isinstance(t, SimulatedNode) and t.telemetry is None and isinstance(backends.get(h), StubBackend):
+                t.telemetry = backends[h]
         self.services: list[Service] = []
         self._topology_cache: dict = {}
         self._lock = threading.Lock()
@@ -115,14 +123,16 @@ class Daemon:
         for s in self.services:
             if s.is_alive():
                 s.join(timeout)
-        for b in set(map(id, self.backends.values())):
-            pass
         for b in {id(b): b for b in self.backends.values()}.values():
             try:
                 b.close()
             except Exception:  # noqa: BLE001
                 pass
         self.transports.close()
+        from . import task_nursery
+
+        if task_nursery._transports is self.transports:
+            task_nursery.use_transports(None)
 
     def wake(self, reason: str = "") -> None:
         """Event-driven wake-up of the job scheduler (enqueue, reservation change, job stop)."""

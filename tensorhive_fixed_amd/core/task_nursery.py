@@ -54,12 +54,25 @@ def _th_run(host: str) -> str:
     return get_config().launcher.supervisor
 
 
+_transports: TransportManager | None = None
+
+
+def use_transports(tm: TransportManager | None) -> None:
+    """Route task operations through the daemon's transports (set by :class:`Daemon`)."""
+    global _transports
+    _transports = tm
+
+
 def _client(host: str, user: str) -> TransportManager:
     return ssh.get_client(*ssh.build_dedicated_config_for(host, user))
 
 
 def _run(host: str, user: str, cmd: str, timeout: float | None = None) -> Result:
-    return _client(host, user).run(host, cmd, timeout=timeout or get_config().ssh.timeout + 20)
+    timeout = timeout or get_config().ssh.timeout + 20
+    tm = _transports
+    if tm is not None and host in tm.transports:
+        return tm.get(host).run(cmd, timeout=timeout, user=user)
+    return _client(host, user).run(host, cmd, timeout=timeout)
 
 
 def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | None = None) -> str:

@@ -254,7 +254,7 @@ class StubBackend(TelemetryBackend):
                         "hotspot_temp": _metric(45 + util * 0.4, "C"), "mem_temp": _metric(40 + util * 0.2, "C"),
                         "gfx_clock": _metric(2400 if busy else 150, "MHz"), "mem_clock": _metric(2000, "MHz"),
                         "xgmi_read": _metric(0.0, "GB/s"), "xgmi_write": _metric(0.0, "GB/s"),
-                        "energy": _metric(180 + util * 8, "W"),
+                        "energy": _metric(180 + util * 8, "W"),  # accumulator-derived power, as libthsmi
                     },
                     "processes": procs,
                 }

@@ -10,6 +10,9 @@ cached per-host clients, optional proxy jump) and ``core/ssh.py`` (``run_command
   session per host and user, reused by every command: no per-command handshake), optional
   ProxyJump, BatchMode, TensorHive's dedicated key.
 * :class:`FakeTransport` -- scripted replies + fault injection (drop host, hang, fail) for tests.
+* :class:`SimulatedNode` -- a node that understands the ``th-run`` protocol in-process (spawn,
+  ls, signals, logs) and shows spawned tasks as GPU processes in a :class:`StubBackend`; used by
+  the CPU test-suite, demos and the daemon benchmarks (``transport = simulated``).
 * :class:`TransportManager` -- per-host transports from ``hosts_config.ini`` and a thread-pool
   fan-out (``run_all``) whose per-host failures never abort the others.
 """
@@ -17,6 +20,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import getpass
+import json
 import logging
 import os
 import re
@@ -156,6 +160,94 @@ class FakeTransport(Transport):
         return Result(self.host, "", f"no rule for: {command}", 127)
 
 
+class SimulatedNode(FakeTransport):
+    """In-process node speaking the ``th-run`` protocol (see ``native/th_run.cpp``).
+
+    Spawned tasks get a fresh pid; when ``telemetry`` (a StubBackend) is given they appear on the
+    GPUs named by ``HIP_VISIBLE_DEVICES`` with their owner and ``TENSORHIVE_TASK_ID``, exactly as
+    the amdsmi backend would report them.  ``exit_task(pid)`` simulates a task finishing."""
+
+    _SPAWN = re.compile(r"spawn --name (\S+) --log (\S+)((?: --env \S+)*) -- bash -lc (.*?); else")
+    _SIG = re.compile(r"then \S+ (interrupt|terminate|kill) --pid (\d+)")
+
+    def __init__(self, host: str, telemetry=None, first_pid: int = 40000):
+        super().__init__(host)
+        self.telemetry = telemetry
+        self.sessions: dict[int, dict] = {}
+        self.logs: dict[str, list[str]] = {}
+        self._next = first_pid
+
+    def run(self, command, timeout=None, user=None, env=None) -> Result:
+        with self._lock:
+            self.calls.append((command, user))
+        if self.down:
+            return Result(self.host, "", "host unreachable", 255, ConnectionError("host unreachable"))
+        for pat, fn in self.rules:  # explicit rules win (fault injection)
+            if pat.search(command):
+                out, err, rc = fn(command, user)
+                return Result(self.host, out, err, rc)
+        m = self._SPAWN.search(command)
+        if m:
+            return self._spawn(m, user)
+        m = self._SIG.search(command)
+        if m:
+            return self._signal(int(m.group(2)), m.group(1), user)
+        if re.search(r"then \S+ ls; fi", command):
+            with self._lock:
+                lines = [json.dumps({k: v for k, v in s.items() if k != "gpus"}) for s in self.sessions.values()
+                         if s["user"] == user]
+            return Result(self.host, "\n".join(lines) + ("\n" if lines else ""), "", 0)
+        m = re.match(r"(?:tail -n (\d+)|cat) (\S+)$", command.strip())
+        if m:
+            lines = self.logs.get(m.group(2))
+            if lines is None:
+                return Result(self.host, "", "No such file", 1)
+            lines = lines[-int(m.group(1)):] if m.group(1) else lines
+            return Result(self.host, "".join(l + "\n" for l in lines), "", 0)
+        if command.strip() == "uname":
+            return Result(self.host, "Linux\n", "", 0)
+        return Result(self.host, "", f"simulated node: unsupported command {command[:80]}", 127)
+
+    def _spawn(self, m, user) -> Result:
+        name, logf, envs, cmd = m.group(1), m.group(2), m.group(3), m.group(4)
+        env = dict(shlex.split(e)[0].split("=", 1) for e in re.findall(r"--env (\S+)", envs))
+        cmd = shlex.split(cmd)[0] if cmd.startswith("'") else cmd
+        gpus = []
+        mv = re.search(r"(?:HIP|ROCR)_VISIBLE_DEVICES=([0-9,]+)", cmd)
+        if mv:
+            gpus = [int(x) for x in mv.group(1).split(",") if x]
+        with self._lock:
+            pid = self._next
+            self._next += 1
+            self.sessions[pid] = {"name": name, "pid": pid, "pgid": pid, "started": time.time(), "user": user,
+                                  "command": cmd, "log": logf, "gpus": gpus}
+            self.logs[logf] = [f"[simulated] {cmd}"]
+        if self.telemetry is not None:
+            for g in gpus:
+                self.telemetry.add_process(self.host, g, pid, user or "", cmd[:80], env.get("TENSORHIVE_TASK_ID"))
+        return Result(self.host, f"{pid}\n", "", 0)
+
+    def exit_task(self, pid: int, line: str = "[simulated] done") -> None:
+        with self._lock:
+            s = self.sessions.pop(pid, None)
+        if s is None:
+            return
+        self.logs.setdefault(s["log"], []).append(line)
+        if self.telemetry is not None:
+            with self.telemetry._lock:
+                for k, procs in list(self.telemetry.processes.items()):
+                    if k[0] == self.host:
+                        self.telemetry.processes[k] = [p for p in procs if p["pid"] != pid]
+
+    def _signal(self, pid: int, verb: str, user) -> Result:
+        with self._lock:
+            s = self.sessions.get(pid)
+        if s is None or (user and s["user"] != user):
+            return Result(self.host, "", f"no such session {pid}", 1)
+        self.exit_task(pid, f"[simulated] {verb}")
+        return Result(self.host, "", "", 0)
+
+
 @dataclass
 class TransportManager:
     """Per-host transports + parallel fan-out (``stop_on_errors=False`` semantics)."""
@@ -171,6 +263,8 @@ class TransportManager:
             kind = spec.get("transport", "ssh")
             if kind == "local" or (kind == "auto" and host in ("localhost", "127.0.0.1")):
                 tm.transports[host] = LocalTransport(host, spec.get("user"))
+            elif kind == "simulated":
+                tm.transports[host] = SimulatedNode(host)
             else:
                 tm.transports[host] = SSHTransport(host, spec.get("user") or getpass.getuser(),
                                                    int(spec.get("port", 22)), key_file, proxy, timeout)

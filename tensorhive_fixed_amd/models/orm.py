@@ -47,6 +47,14 @@ def _utcnow():
 
 
 # ------------------------------------------------------------------------------------ users
+def _refresh_view(obj, attr: str) -> None:
+    """The reverse side of a many-to-many is ``viewonly``: reload it after the owning side changed."""
+    from sqlalchemy import inspect as sa_inspect
+
+    if sa_inspect(obj).persistent:
+        db_session.expire(obj, [attr])
+
+
 class User2Group(Base):
     __tablename__ = "user2group"
     user_id = Column(Integer, ForeignKey("users.id", ondelete="CASCADE"), primary_key=True)
@@ -288,12 +296,14 @@ class Group(CRUDModel, RestrictionAssignee, Base):
             raise InvalidRequestException(f"User {user} is already a member of group {self}!")
         self._users.append(user)
         self.save()
+        _refresh_view(user, "_groups")
 
     def remove_user(self, user):
         if user not in self._users:
             raise InvalidRequestException(f"User {user} is not a member of group {self}!")
         self._users.remove(user)
         self.save()
+        _refresh_view(user, "_groups")
 
     def as_dict(self, include_private=False, include_users=True):
         d = super().as_dict(include_private)
@@ -478,12 +488,14 @@ class Restriction(CRUDModel, Base):
             raise InvalidRequestException(f"Restriction {self} is already being applied to {what} {item}")
         coll.append(item)
         self.save()
+        _refresh_view(item, "_restrictions")
 
     def _remove(self, coll, item, what):
         if item not in coll:
             raise InvalidRequestException(f"{what} {item} is not affected by restriction {self}")
         coll.remove(item)
         self.save()
+        _refresh_view(item, "_restrictions")
 
     def apply_to_user(self, user):
         self._add(self._users, user, "user")
@@ -857,6 +869,7 @@ class Task(CRUDModel, Base):
             (envs if lk.segment.segment_type == SegmentType.env_variable else params).append(seg)
         d["cmdsegments"] = {"envs": envs, "params": params}
         d["fullCommand"] = self.full_command
+        d["gpuId"] = self.gpu_id  # additive: first device of HIP_VISIBLE_DEVICES
         return d
 
 
@@ -966,6 +979,7 @@ class Job(CRUDModel, Base):
     def as_dict(self, include_private=None):
         d = super().as_dict(bool(include_private))
         d["status"] = self._status.name
+        d["isQueued"] = bool(self.is_queued)  # additive (dashboard queue badge)
         return d
 
     @staticmethod

@@ -40,17 +40,18 @@ import json  # noqa: E402
 HOSTS_INI = """
 [node-a]
 user = tester
-transport = local
+transport = simulated
 
 [node-b]
 user = tester
-transport = local
+transport = simulated
 """
 
 
 @pytest.fixture()
 def cfg(tmp_path, monkeypatch):
-    """A private config dir (2 local 'nodes'), in-memory DB, installed as the global config."""
+    """A private config dir (2 simulated MI355X nodes speaking the th-run protocol in-process),
+    in-memory DB, installed as the global config."""
     from tensorhive_fixed_amd import config as C
 
     monkeypatch.setenv("TENSORHIVE_CONFIG_DIR", str(tmp_path))
@@ -102,7 +103,9 @@ def daemon(cfg, tables):
 def app(daemon):
     from tensorhive_fixed_amd.api.app import create_app
 
-    return create_app(daemon)
+    a = create_app(daemon)
+    a.config["TH_REMOVE_SESSION"] = False
+    return a
 
 
 @pytest.fixture()
@@ -152,9 +155,162 @@ def resource1(tables):
 def permissive_restriction(tables):
     from tensorhive_fixed_amd.models.orm import Restriction
 
-    r = Restriction(name="everything", starts_at=datetime.datetime.utcnow() - datetime.timedelta(days=1),
+    r = Restriction(name="everything", starts_at=datetime.datetime.utcnow() - datetime.timedelta(days=10),
                     is_global=True)
     r.save()
     return r
 
 
+
+
+# ----------------------------------------------------------------------------- model fixtures
+# Same scenarios as the reference's tests/fixtures/models.py (users, GPUs, restrictions, schedules,
+# reservations, jobs, tasks); values chosen independently.
+def _in(**kw):
+    return datetime.datetime.utcnow() + datetime.timedelta(**kw)
+
+
+@pytest.fixture()
+def new_user_2(tables):
+    return _mk_user("AnotherUser")
+
+
+@pytest.fixture()
+def resource2(tables):
+    from tensorhive_fixed_amd.models.orm import Resource
+
+    r = Resource(id="GPU-" + "1" * 36, name="Custom name", hostname="node-b")
+    r.save()
+    return r
+
+
+@pytest.fixture()
+def restriction(tables):
+    from tensorhive_fixed_amd.models.orm import Restriction
+
+    start = _in(minutes=5)
+    r = Restriction(name="TestRestriction", starts_at=start, ends_at=start + datetime.timedelta(hours=8))
+    r.save()
+    return r
+
+
+@pytest.fixture()
+def new_group(tables):
+    from tensorhive_fixed_amd.models.orm import Group
+
+    return Group(name="TestGroup1")
+
+
+@pytest.fixture()
+def new_group_with_member(tables, new_user):
+    from tensorhive_fixed_amd.models.orm import Group
+
+    g = Group(name="TestGroup1")
+    g.save()
+    g.add_user(new_user)
+    return g
+
+
+def _schedule(days, a, b):
+    from tensorhive_fixed_amd.models.orm import RestrictionSchedule
+
+    s = RestrictionSchedule(schedule_days=days, hour_start=a, hour_end=b)
+    s.save()
+    return s
+
+
+@pytest.fixture()
+def active_schedule(tables):
+    return _schedule("1234567", datetime.time(0, 0), datetime.time(23, 59, 59))
+
+
+@pytest.fixture()
+def inactive_schedule(tables):
+    today = str(datetime.datetime.utcnow().weekday() + 1)
+    return _schedule("1234567".replace(today, ""), datetime.time(8, 0), datetime.time(10, 0))
+
+
+def _reservation(user, res, start, dur):
+    from tensorhive_fixed_amd.models.orm import Reservation
+
+    return Reservation(user_id=user.id, title="TEST TITLE", description="TEST_DESCRIPTION", resource_id=res.id,
+                       start=start, end=start + dur)
+
+
+@pytest.fixture()
+def new_reservation(new_user, resource1):
+    return _reservation(new_user, resource1, datetime.datetime.utcnow(), datetime.timedelta(minutes=60))
+
+
+@pytest.fixture()
+def new_reservation_2(new_user, new_admin, resource1):
+    return _reservation(new_admin, resource1, datetime.datetime.utcnow(), datetime.timedelta(minutes=60))
+
+
+@pytest.fixture()
+def past_reservation(new_user, resource1):
+    return _reservation(new_user, resource1, _in(hours=-5), datetime.timedelta(minutes=60))
+
+
+@pytest.fixture()
+def active_reservation(new_user, resource1):
+    return _reservation(new_user, resource1, _in(hours=-5), datetime.timedelta(hours=10))
+
+
+@pytest.fixture()
+def future_reservation(new_user, resource1):
+    return _reservation(new_user, resource1, _in(hours=5), datetime.timedelta(hours=10))
+
+
+@pytest.fixture()
+def new_task(tables):
+    from tensorhive_fixed_amd.models.orm import CommandSegment, SegmentType, Task, TaskStatus
+
+    t = Task(command="python train.py", hostname="node-a", _status=TaskStatus.not_running)
+    t.add_cmd_segment(CommandSegment(name="--batch_size", segment_type=SegmentType.parameter), "32")
+    t.save()
+    return t
+
+
+@pytest.fixture()
+def new_task_2(tables):
+    from tensorhive_fixed_amd.models.orm import CommandSegment, SegmentType, Task, TaskStatus
+
+    t = Task(command="python eval.py", hostname="node-b", _status=TaskStatus.not_running)
+    t.add_cmd_segment(CommandSegment(name="HIP_VISIBLE_DEVICES", segment_type=SegmentType.env_variable), "0")
+    t.save()
+    return t
+
+
+def _job(user, name="job_name", status=None):
+    from tensorhive_fixed_amd.models.orm import Job, JobStatus
+
+    j = Job(name=name, description="testDescription", user_id=user.id, status=status or JobStatus.not_running)
+    j.save()
+    return j
+
+
+@pytest.fixture()
+def new_job(new_user):
+    return _job(new_user)
+
+
+@pytest.fixture()
+def new_running_job(new_user):
+    from tensorhive_fixed_amd.models.orm import JobStatus
+
+    return _job(new_user, "running_job", JobStatus.running)
+
+
+@pytest.fixture()
+def new_job_with_task(new_user, new_task):
+    j = _job(new_user)
+    j.add_task(new_task)
+    return j
+
+
+@pytest.fixture()
+def new_admin_job(new_user, new_admin, new_task):
+    j = _job(new_admin, "admin_job")
+    j.add_task(new_task)
+    return j
