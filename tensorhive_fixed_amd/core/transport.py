@@ -175,6 +175,9 @@ class SimulatedNode(FakeTransport):
         self.telemetry = telemetry
         self.sessions: dict[int, dict] = {}
         self.logs: dict[str, list[str]] = {}
+        self.ttys: list[tuple[str, str]] = []  # (user, tty) pairs reported by `who`
+        self.tty_messages: list[tuple[str, str]] = []  # (tty, text) written by warnings
+        self.killed: list[tuple[int, str | None, bool]] = []  # (pid, as user, via sudo)
         self._next = first_pid
 
     def run(self, command, timeout=None, user=None, env=None) -> Result:
@@ -206,7 +209,29 @@ class SimulatedNode(FakeTransport):
             return Result(self.host, "".join(l + "\n" for l in lines), "", 0)
         if command.strip() == "uname":
             return Result(self.host, "Linux\n", "", 0)
+        if command.strip() == "who":
+            return Result(self.host, "".join(f"{u} {t} 2026-01-01 00:00\n" for u, t in self.ttys), "", 0)
+        if "| tee /dev/" in command:
+            for text, tty in re.findall(r"echo -e (.*?) \| tee /dev/(\S+) >/dev/null", command, re.S):
+                self.tty_messages.append((tty, shlex.split(text)[0] if text.startswith("'") else text))
+            return Result(self.host, "", "", 0)
+        m = re.match(r"(sudo -n )?kill ((?:\d+ ?)+)$", command.strip())
+        if m:
+            for pid in map(int, m.group(2).split()):
+                self.killed.append((pid, user, bool(m.group(1))))
+                self._drop_gpu_process(pid)
+                with self._lock:
+                    self.sessions.pop(pid, None)
+            return Result(self.host, "", "", 0)
         return Result(self.host, "", f"simulated node: unsupported command {command[:80]}", 127)
+
+    def _drop_gpu_process(self, pid: int) -> None:
+        if self.telemetry is None:
+            return
+        with self.telemetry._lock:
+            for k, procs in list(self.telemetry.processes.items()):
+                if k[0] == self.host:
+                    self.telemetry.processes[k] = [p for p in procs if p["pid"] != pid]
 
     def _spawn(self, m, user) -> Result:
         name, logf, envs, cmd = m.group(1), m.group(2), m.group(3), m.group(4)
@@ -233,11 +258,7 @@ class SimulatedNode(FakeTransport):
         if s is None:
             return
         self.logs.setdefault(s["log"], []).append(line)
-        if self.telemetry is not None:
-            with self.telemetry._lock:
-                for k, procs in list(self.telemetry.processes.items()):
-                    if k[0] == self.host:
-                        self.telemetry.processes[k] = [p for p in procs if p["pid"] != pid]
+        self._drop_gpu_process(pid)
 
     def _signal(self, pid: int, verb: str, user) -> Result:
         with self._lock:

@@ -158,8 +158,7 @@ class UserProcessKillingBehaviour:
         for host, pids in violation_data["VIOLATION_PIDS"].items():
             cmd = "kill " + " ".join(str(int(p)) for p in sorted(pids))
             try:
-                client = ssh.get_client(*ssh.build_dedicated_config_for(host, user))
-                r = client.run(host, cmd)
+                r = self.transports.get(host).run(cmd, user=user)
                 log.warning("killed %s of %s on %s (rc=%s)", sorted(pids), user, host, r.exit_code)
             except Exception as e:  # noqa: BLE001
                 log.error("unable to kill processes of %s on %s: %s", user, host, e)

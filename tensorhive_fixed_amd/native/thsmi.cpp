@@ -7,10 +7,13 @@
 // fan_speed = null on the passively cooled MI355X) plus MI355X extras (hotspot/HBM temperature,
 // gfx/mem clocks, energy, xGMI read/write throughput from the PMFW accumulators), and the GPU's
 // processes already attributed to a UNIX owner and -- via /proc/<pid>/environ -- to the
-// TensorHive task that launched them (TENSORHIVE_TASK_ID).  Processes come from amdsmi and are
-// cross-checked with KFD sysfs (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>), which also covers
-// containers where amdsmi cannot see host PIDs.  CPU utilisation is a /proc/stat delta between
-// two calls (no `sleep 1`).
+// TensorHive task that launched them (TENSORHIVE_TASK_ID).  Process discovery has two sources:
+//   * amdsmi + KFD sysfs (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>) -- these are HOST pids;
+//     a pid is only trusted when the process it names in OUR /proc really has /dev/kfd open
+//     (inside a container, a host pid may be absent or name an unrelated process);
+//   * DRM fdinfo of the amdgpu render nodes (/proc/<pid>/fdinfo/<fd>: drm-pdev, drm-client-id,
+//     drm-memory-vram) -- pids of our own PID namespace, per device BDF, with VRAM.
+// CPU utilisation is a /proc/stat delta between two calls (no `sleep 1`).
 //
 // C ABI (ctypes):  thsmi_init() -> 0 | <0,  thsmi_sample_json(buf, cap) -> bytes | -needed,
 //                  thsmi_topology_json(buf, cap), thsmi_shutdown().
@@ -149,6 +152,73 @@ std::map<uint64_t, std::set<long>> kfd_processes() {
   return out;
 }
 
+// does /proc/<pid>/fd contain an open /dev/kfd?  (same-uid or root can read the links)
+bool has_kfd_open(long pid) {
+  const std::string fdd = "/proc/" + std::to_string(pid) + "/fd";
+  DIR* d = opendir(fdd.c_str());
+  if (!d) return false;
+  bool found = false;
+  char tgt[256];
+  struct dirent* e;
+  while (!found && (e = readdir(d)) != nullptr) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    const std::string l = fdd + "/" + e->d_name;
+    ssize_t n = readlink(l.c_str(), tgt, sizeof tgt - 1);
+    if (n > 0) {
+      tgt[n] = 0;
+      found = strcmp(tgt, "/dev/kfd") == 0;
+    }
+  }
+  closedir(d);
+  return found;
+}
+
+// DRM fdinfo scan: bdf -> pid -> VRAM bytes (summed over distinct drm clients of the process)
+std::map<std::string, std::map<long, uint64_t>> drm_processes() {
+  std::map<std::string, std::map<long, uint64_t>> out;
+  DIR* pd = opendir("/proc");
+  if (!pd) return out;
+  struct dirent* pe;
+  char tgt[256];
+  while ((pe = readdir(pd)) != nullptr) {
+    if (pe->d_name[0] < '0' || pe->d_name[0] > '9') continue;
+    const long pid = atol(pe->d_name);
+    const std::string base = std::string("/proc/") + pe->d_name;
+    DIR* fd = opendir((base + "/fd").c_str());
+    if (!fd) continue;
+    std::set<std::string> clients;
+    struct dirent* fe;
+    while ((fe = readdir(fd)) != nullptr) {
+      if (fe->d_name[0] < '0' || fe->d_name[0] > '9') continue;
+      const std::string l = base + "/fd/" + fe->d_name;
+      ssize_t n = readlink(l.c_str(), tgt, sizeof tgt - 1);
+      if (n <= 0) continue;
+      tgt[n] = 0;
+      if (strncmp(tgt, "/dev/dri/renderD", 16) != 0) continue;
+      std::string info = read_file(base + "/fdinfo/" + fe->d_name, 8192);
+      const char* pdev = strstr(info.c_str(), "drm-pdev:");
+      if (!pdev) continue;
+      char bdf[32] = {0};
+      sscanf(pdev + 9, " %31s", bdf);
+      const char* cid = strstr(info.c_str(), "drm-client-id:");
+      std::string key = std::string(bdf) + "#" + (cid ? std::to_string(strtoull(cid + 14, nullptr, 10)) : fe->d_name);
+      if (!clients.insert(key).second) continue;  // dup'ed fd of the same client
+      uint64_t vram = 0;
+      const char* vm = strstr(info.c_str(), "drm-memory-vram:");
+      if (vm) {
+        char unit[8] = {0};
+        unsigned long long v = 0;
+        sscanf(vm + 16, " %llu %7s", &v, unit);
+        vram = v * (unit[0] == 'K' ? 1024ull : unit[0] == 'M' ? 1048576ull : unit[0] == 'G' ? 1073741824ull : 1ull);
+      }
+      out[bdf][pid] += vram;
+    }
+    closedir(fd);
+  }
+  closedir(pd);
+  return out;
+}
+
 std::string cpu_json() {
   std::string st = read_file("/proc/stat", 4096);
   unsigned long long v[10] = {0};
@@ -228,7 +298,8 @@ int discover() {
   return (int)g_gpus.size();
 }
 
-std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd, uint64_t ts) {
+std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd,
+                     const std::map<std::string, std::map<long, uint64_t>>& drm, uint64_t ts) {
   amdsmi_engine_usage_t act;
   memset(&act, 0, sizeof act);
   const bool act_ok = amdsmi_get_gpu_activity(g.h, &act) == AMDSMI_STATUS_SUCCESS;
@@ -287,17 +358,24 @@ std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd, uint
   m += ",\"energy\":" + metric("W", e_rate >= 0, e_rate);
   m += "}";
 
-  std::map<long, uint64_t> procs;  // pid -> vram bytes
+  std::map<long, uint64_t> host;  // amdsmi / KFD: host pid -> vram bytes
   uint32_t np = 0;
   if (amdsmi_get_gpu_process_list(g.h, &np, nullptr) == AMDSMI_STATUS_SUCCESS && np) {
     std::vector<amdsmi_proc_info_t> pl(np);
     if (amdsmi_get_gpu_process_list(g.h, &np, pl.data()) == AMDSMI_STATUS_SUCCESS)
-      for (uint32_t i = 0; i < np; ++i) procs[(long)pl[i].pid] = pl[i].memory_usage.vram_mem;
+      for (uint32_t i = 0; i < np; ++i) host[(long)pl[i].pid] = pl[i].memory_usage.vram_mem;
   }
   auto it = kfd.find(g.kfd_id);
   if (it != kfd.end())
     for (long pid : it->second)
-      if (!procs.count(pid)) procs[pid] = 0;
+      if (!host.count(pid)) host[pid] = 0;
+  std::map<long, uint64_t> procs;  // pids of our namespace
+  for (const auto& p : host)
+    if (has_kfd_open(p.first)) procs[p.first] = p.second;
+  auto dit = drm.find(g.bdf);
+  if (dit != drm.end())
+    for (const auto& p : dit->second)
+      if (p.second > 0 || procs.count(p.first)) procs[p.first] = std::max(procs[p.first], p.second);
   std::string ps = "[";
   bool first = true;
   for (const auto& p : procs) {
@@ -344,8 +422,9 @@ extern "C" int thsmi_sample_json(char* buf, int cap) {
   if (!g_init) return -1000000000;
   const uint64_t ts = now_ns();
   auto kfd = kfd_processes();
+  auto drm = drm_processes();
   std::string s = "{\"ts_ns\":" + std::to_string(ts) + ",\"cpu\":" + cpu_json() + ",\"gpus\":[";
-  for (size_t i = 0; i < g_gpus.size(); ++i) s += (i ? "," : "") + gpu_json(g_gpus[i], kfd, ts);
+  for (size_t i = 0; i < g_gpus.size(); ++i) s += (i ? "," : "") + gpu_json(g_gpus[i], kfd, drm, ts);
   s += "]}";
   return emit(s, buf, cap);
 }

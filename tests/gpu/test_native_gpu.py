@@ -1,0 +1,135 @@
+"""Native node-side components on a real MI355X: libthsmi (amdsmi + KFD process attribution),
+the th-smi CLI, the gfx950 probe kernel, and the daemon's local telemetry path end to end."""
+import getpass
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r"""
+import sys, time, torch
+x = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")   # 256 MiB resident
+x.fill_(1); torch.cuda.synchronize()
+print("ready", flush=True)
+time.sleep(float(sys.argv[1]))
+"""
+
+
+@pytest.fixture(scope="module")
+def backend():
+    from tensorhive_fixed_amd.core.telemetry import AmdSmiBackend
+
+    b = AmdSmiBackend()
+    yield b
+    b.close()
+
+
+def test_thsmi_inventory(backend):
+    entry = backend.sample("localhost")
+    gpus = entry["GPU"]
+    assert len(gpus) >= 1 and backend.n_gpus == len(gpus)
+    for uuid, g in gpus.items():
+        assert uuid.startswith("GPU-") and len(uuid) == 40
+        assert "MI355" in (g["name"] or "") or g["name"]
+        m = g["metrics"]
+        for k in ("utilization", "mem_used", "mem_total", "power", "temp"):
+            assert k in m
+        assert m["mem_total"]["value"] > 250_000  # 288 GB HBM3E (MiB)
+    topo = backend.topology("localhost")
+    assert topo["gpus"][0]["bdf"]
+
+
+def test_thsmi_attributes_gpu_processes_to_tasks(backend):
+    env = {**os.environ, "TENSORHIVE_TASK_ID": "4242"}
+    p = subprocess.Popen([sys.executable, "-c", CHILD, "60"], env=env, stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().strip() == "ready"
+        found = None
+        for _ in range(20):
+            for uuid, g in backend.sample("localhost")["GPU"].items():
+                for proc in g["processes"]:
+                    if proc["pid"] == p.pid:
+                        found = proc
+            if found:
+                break
+            time.sleep(0.5)
+        if found is None:
+            diag = {"child": p.pid, "kfd_pids": sorted(os.listdir("/sys/class/kfd/kfd/proc"))
+                    if os.path.isdir("/sys/class/kfd/kfd/proc") else None}
+            fds = {}
+            for fd in os.listdir(f"/proc/{p.pid}/fd"):
+                try:
+                    tgt = os.readlink(f"/proc/{p.pid}/fd/{fd}")
+                except OSError:
+                    continue
+                if tgt.startswith("/dev/dri") or tgt == "/dev/kfd":
+                    info = open(f"/proc/{p.pid}/fdinfo/{fd}").read()
+                    fds[fd] = (tgt, [l for l in info.splitlines() if l.startswith("drm-")][:8])
+            diag["fds"] = fds
+            diag["reported"] = {g["index"]: [x["pid"] for x in g["processes"]]
+                                for g in backend.sample("localhost")["GPU"].values()}
+            raise AssertionError(f"child GPU process not reported: {diag}")
+        assert found["task_id"] == "4242" and found["owner"] == getpass.getuser()
+        assert (found["vram"] or 0) >= 200 << 20 or found["vram"] is None
+    finally:
+        p.kill()
+        p.wait()
+
+
+def test_th_smi_cli():
+    from tensorhive_fixed_amd.native.build import build_all, path_of
+
+    build_all(strict=False)
+    out = subprocess.run([str(path_of("th-smi"))], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    doc = json.loads(out.stdout.strip().splitlines()[-1])
+    assert doc["gpus"] and "cpu" in doc
+    topo = subprocess.run([str(path_of("th-smi")), "--topology"], capture_output=True, text=True, timeout=60)
+    assert json.loads(topo.stdout)["gpus"]
+
+
+def test_probe_kernel_reports_every_xcd():
+    from tensorhive_fixed_amd.core.telemetry import GpuProbe
+
+    probe = GpuProbe(period=0.0, n_wg=64)
+    rows = probe.sample_raw()
+    assert len(rows) == 64
+    assert {r["xcc"] for r in rows} <= set(range(8)) and len({r["xcc"] for r in rows}) >= 2
+    assert all(r["mfma_us"] > 0 and r["hbm_GBps"] > 0 for r in rows)
+    m = probe.maybe_sample()[0]
+    assert 0.0 <= m["mfma_busy"]["value"] <= 100.0
+
+
+def test_daemon_with_local_amdsmi_backend(tmp_path, monkeypatch):
+    """Monitoring service on the real backend publishes snapshots the API serves."""
+    from tensorhive_fixed_amd import config as C
+    from tensorhive_fixed_amd.core.daemon import Daemon
+    from tensorhive_fixed_amd.core.services import MonitoringService
+    from tensorhive_fixed_amd.core.telemetry import AmdSmiBackend
+
+    monkeypatch.setenv("TENSORHIVE_CONFIG_DIR", str(tmp_path))
+    C.init_config_files(tmp_path)
+    (tmp_path / "hosts_config.ini").write_text(f"[localhost]\nuser = {getpass.getuser()}\ntransport = local\n")
+    cfg = C.load_config(tmp_path)
+    C.set_config(cfg)
+    b = AmdSmiBackend(probe=True, probe_period=0.2)
+    d = Daemon(cfg, backends={"localhost": b}, init_key=False, test_ssh=False)
+    mon = MonitoringService(0.2, {"localhost": b})
+    d.add_service(mon)
+    d.init()
+    try:
+        for _ in range(50):
+            snap = d.infrastructure.snapshot()
+            if snap.data.get("localhost"):
+                break
+            time.sleep(0.1)
+        gpus = snap.data["localhost"]["GPU"]
+        assert gpus and all("mfma_busy" in g["metrics"] for g in gpus.values() if g["index"] == 0)
+    finally:
+        d.shutdown()
+        C.set_config(None)
