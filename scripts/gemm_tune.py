@@ -1,0 +1,118 @@
+"""Per-shape GEMM survey + TunableOp tuning for the Llama-3-8B training step on one MI355X.
+
+    python scripts/gemm_tune.py survey            # TFLOP/s of every GEMM of the step, default heuristics
+    python scripts/gemm_tune.py tune              # TunableOp: benchmark hipBLASLt/rocBLAS candidates per
+                                                  # shape, write tensorhive_fixed_amd/ops/tuned/gemm_gfx950.csv
+    python scripts/gemm_tune.py check             # survey again with the tuned table loaded (tuning off)
+
+The GEMMs are exactly the ones the payload issues (ops/linear.py, ops/cross_entropy.py):
+forward ``x @ W^T`` (addmm with the residual for wo / w2), input grad ``dy @ W`` and weight grad
+``dy^T @ x`` written into the flat gradient buffer.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+TUNED = ROOT / "tensorhive_fixed_amd" / "ops" / "tuned" / "gemm_gfx950.csv"
+
+T = 16384  # tokens per micro-step (4 x 4096)
+D, HQKV, FF, V = 4096, 6144, 14336, 128256
+CH = 4096  # CE chunk
+
+
+def shapes():
+    """(name, kind, M, N, K, residual) with C[M,N] = A[M,K] @ B[K,N]."""
+    out = []
+    for name, n_out, k_in, res in (("wqkv", HQKV, D, False), ("wo", D, D, True), ("w13", 2 * FF, D, False),
+                                   ("w2", D, FF, True)):
+        out.append((name, "fwd", T, n_out, k_in, res))
+        out.append((name, "dgrad", T, k_in, n_out, False))
+        out.append((name, "wgrad", n_out, k_in, T, False))
+    out.append(("head", "fwd", CH, V, D, False))
+    out.append(("head", "dgrad", CH, D, V, False))
+    out.append(("head", "wgrad", V, D, CH, True))  # accumulated over chunks (beta = 1)
+    return out
+
+
+def make(kind, M, N, K, res, dev):
+    g = torch.Generator(device=dev).manual_seed(0)
+    r = lambda *s: torch.randn(*s, device=dev, dtype=torch.bfloat16, generator=g)  # noqa: E731
+    if kind == "fwd":  # x[M,K] @ W[N,K]^T
+        x, w = r(M, K), r(N, K)
+        c = r(M, N) if res else None
+        return (lambda: torch.addmm(c, x, w.t())) if res else (lambda: torch.mm(x, w.t()))
+    if kind == "dgrad":  # dy[M,K'] @ W[K',N]   (W stored [out, in] = [K, N])
+        dy, w = r(M, K), r(K, N)
+        return lambda: torch.mm(dy, w)
+    # wgrad: dy^T[N_out, T] @ x[T, K_in] -> out [M=N_out, N=K_in]
+    dy, x = r(K, M), r(K, N)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    if res:
+        return lambda: out.addmm_(dy.t(), x)
+    return lambda: torch.mm(dy.t(), x, out=out)
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def survey(tag):
+    dev = torch.device("cuda:0")
+    tot_ms, tot_fl = 0.0, 0.0
+    rows = []
+    for name, kind, M, N, K, res in shapes():
+        fn = make(kind, M, N, K, res, dev)
+        ms = timeit(fn)
+        fl = 2.0 * M * N * K
+        per_step = 32 if name != "head" else T // CH
+        tot_ms += ms * per_step
+        tot_fl += fl * per_step
+        rows.append({"gemm": f"{name}.{kind}", "M": M, "N": N, "K": K, "ms": round(ms, 4),
+                     "tflops": round(fl / ms / 1e9, 1)})
+        print(json.dumps(rows[-1]), flush=True)
+    print(json.dumps({"tag": tag, "gemm_ms_per_step": round(tot_ms, 1), "avg_tflops": round(tot_fl / tot_ms / 1e9, 1)}),
+          flush=True)
+
+
+def main():
+    mode = sys.argv[1] if len(sys.argv) > 1 else "survey"
+    tun = torch.cuda.tunable
+    if mode == "tune":
+        TUNED.parent.mkdir(parents=True, exist_ok=True)
+        if TUNED.exists():
+            TUNED.unlink()
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_filename(str(TUNED))
+        tun.set_max_tuning_duration(int(os.environ.get("TH_TUNE_MS", "400")))
+        t0 = time.time()
+        survey("tuning-pass")
+        tun.write_file()
+        print(json.dumps({"tuned_file": str(TUNED), "tuning_s": round(time.time() - t0, 1)}))
+        return
+    if mode == "check":
+        tun.enable(True)
+        tun.tuning_enable(False)
+        tun.set_filename(str(TUNED))
+        tun.read_file(str(TUNED))
+    survey(mode)
+
+
+if __name__ == "__main__":
+    main()

@@ -248,10 +248,15 @@ int do_spawn(Args& a) {
   pid_t p2 = fork();
   if (p2 < 0) _exit(1);
   if (p2 > 0) _exit(0);
-  // monitor process
-  signal(SIGINT, SIG_IGN);
-  signal(SIGTERM, SIG_IGN);
-  signal(SIGHUP, SIG_IGN);
+  // monitor process.  INT/TERM/HUP stay BLOCKED across the fork below: the task child resets them
+  // to SIG_DFL before unblocking (a signal sent the moment its pid is known is then delivered with
+  // the default action instead of being lost to an inherited SIG_IGN); the monitor ignores them.
+  sigset_t guard, prev;
+  sigemptyset(&guard);
+  sigaddset(&guard, SIGINT);
+  sigaddset(&guard, SIGTERM);
+  sigaddset(&guard, SIGHUP);
+  sigprocmask(SIG_BLOCK, &guard, &prev);
   signal(SIGPIPE, SIG_IGN);
   int out[2];
   if (pipe(out) != 0) _exit(1);
@@ -265,6 +270,7 @@ int do_spawn(Args& a) {
     signal(SIGTERM, SIG_DFL);
     signal(SIGHUP, SIG_DFL);
     signal(SIGPIPE, SIG_DFL);
+    sigprocmask(SIG_SETMASK, &prev, nullptr);
     dup2(out[1], 1);
     dup2(out[1], 2);
     close(out[0]);
@@ -286,6 +292,10 @@ int do_spawn(Args& a) {
     _exit(127);
   }
   setpgid(c, c);  // race-free: both sides set it
+  signal(SIGINT, SIG_IGN);
+  signal(SIGTERM, SIG_IGN);
+  signal(SIGHUP, SIG_IGN);
+  sigprocmask(SIG_SETMASK, &prev, nullptr);
   close(out[1]);
   KV st;
   st["name"] = a.name;

@@ -25,13 +25,25 @@ def timeit(func):
     return wrapper
 
 
+def _freeze(v):
+    """Hashable stand-in for dict/list/set arguments (the reference keyed on ``str(args)``)."""
+    if isinstance(v, dict):
+        return ("dict", tuple(sorted((k, _freeze(x)) for k, x in v.items())))
+    if isinstance(v, (list, tuple)):
+        return (type(v).__name__, tuple(_freeze(x) for x in v))
+    if isinstance(v, (set, frozenset)):
+        return ("set", tuple(sorted(map(repr, v))))
+    return v
+
+
 def memoize(func):
     cache: dict = {}
     lock = threading.Lock()
 
     @functools.wraps(func)
     def wrapper(*args, **kwargs):
-        key = (tuple((a, type(a)) for a in args), tuple(sorted((k, v, type(v)) for k, v in kwargs.items())))
+        key = (tuple((_freeze(a), type(a)) for a in args),
+               tuple(sorted((k, _freeze(v), type(v)) for k, v in kwargs.items())))
         with lock:
             if key in cache:
                 return cache[key]
