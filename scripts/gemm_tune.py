@@ -3,6 +3,7 @@
     python scripts/gemm_tune.py survey            # TFLOP/s of every GEMM of the step, default heuristics
     python scripts/gemm_tune.py tune              # TunableOp: benchmark hipBLASLt/rocBLAS candidates per
                                                   # shape, write tensorhive_fixed_amd/ops/tuned/gemm_gfx950.csv
+    python scripts/gemm_tune.py resume            # tune only the shapes missing from the table
     python scripts/gemm_tune.py check             # survey again with the tuned table loaded (tuning off)
 
 The GEMMs are exactly the ones the payload issues (ops/linear.py, ops/cross_entropy.py):
@@ -93,14 +94,17 @@ def survey(tag):
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "survey"
     tun = torch.cuda.tunable
-    if mode == "tune":
+    if mode in ("tune", "resume"):
         TUNED.parent.mkdir(parents=True, exist_ok=True)
-        if TUNED.exists():
+        if mode == "tune" and TUNED.exists():
             TUNED.unlink()
         tun.enable(True)
         tun.tuning_enable(True)
         tun.set_filename(str(TUNED))
+        if mode == "resume" and TUNED.exists():
+            tun.read_file(str(TUNED))  # already-tuned shapes are not tuned again
         tun.set_max_tuning_duration(int(os.environ.get("TH_TUNE_MS", "400")))
+        tun.set_max_tuning_iterations(int(os.environ.get("TH_TUNE_ITERS", "20")))
         t0 = time.time()
         survey("tuning-pass")
         tun.write_file()

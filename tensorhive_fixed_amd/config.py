@@ -229,6 +229,8 @@ class AmdMonitorConfig:
     probe_enabled: bool
     probe_period: float
     stub_gpus: int
+    counters_enabled: bool = False
+    counters_period_ms: int = 1000
 
 
 @dataclass
@@ -389,6 +391,8 @@ def load_config(directory: Path | str | None = None) -> Config:
             probe_enabled=main.bool("amd_monitor", "probe_enabled", False),
             probe_period=main.float("amd_monitor", "probe_period", 1.0),
             stub_gpus=main.int("amd_monitor", "stub_gpus", 8),
+            counters_enabled=main.bool("amd_monitor", "counters_enabled", False),
+            counters_period_ms=main.int("amd_monitor", "counters_period_ms", 1000),
         ),
         launcher=LauncherConfig(
             supervisor=main.str("launcher", "supervisor", "th-run"),

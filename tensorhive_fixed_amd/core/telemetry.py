@@ -69,7 +69,8 @@ class AmdSmiBackend(TelemetryBackend):
 
     name = "amdsmi"
 
-    def __init__(self, probe: bool = False, probe_period: float = 1.0):
+    def __init__(self, probe: bool = False, probe_period: float = 1.0, counters: bool = False,
+                 counters_period_ms: int = 1000):
         if not NATIVE_LIB.exists():
             from ..native.build import build_all
 
@@ -84,6 +85,11 @@ class AmdSmiBackend(TelemetryBackend):
         self._buf = ctypes.create_string_buffer(1 << 20)
         self._lock = threading.Lock()
         self.probe = GpuProbe(probe_period) if probe else None
+        self.counters = None
+        if counters:
+            from .counters import CounterStream
+
+            self.counters = CounterStream(period_ms=counters_period_ms)
 
     def _call(self, fn) -> dict:
         with self._lock:
@@ -95,13 +101,21 @@ class AmdSmiBackend(TelemetryBackend):
 
     def sample(self, host: str) -> dict | None:
         doc = self._call(self.lib.thsmi_sample_json)
-        extra = self.probe.maybe_sample() if self.probe else None
-        return entry_from_thsmi(host, doc, extra)
+        extra = {k: dict(v) for k, v in (self.probe.maybe_sample() or {}).items()} if self.probe else {}
+        if self.counters is not None:
+            by_kfd = self.counters.latest()
+            for g in doc.get("gpus", []):
+                m = by_kfd.get(g.get("kfd_id"))
+                if m:
+                    extra.setdefault(g["index"], {}).update(m)
+        return entry_from_thsmi(host, doc, extra or None)
 
     def topology(self, host: str) -> dict | None:
         return self._call(self.lib.thsmi_topology_json)
 
     def close(self) -> None:
+        if self.counters is not None:
+            self.counters.close()
         self.lib.thsmi_shutdown()
 
 
@@ -271,14 +285,16 @@ class StubBackend(TelemetryBackend):
 
 
 def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, probe: bool = False,
-                 probe_period: float = 1.0, stream_ms: int | None = None) -> TelemetryBackend:
+                 probe_period: float = 1.0, stream_ms: int | None = None, counters: bool = False,
+                 counters_period_ms: int = 1000) -> TelemetryBackend:
     """Pick a backend for ``host``: ``auto`` = amdsmi for the local node when /dev/kfd exists,
     remote th-smi for ssh nodes, stub otherwise."""
     spec_local = transports is None or getattr(transports.transports.get(host), "__class__", None).__name__ == "LocalTransport"
     if kind == "stub":
         return StubBackend(stub_gpus)
     if kind == "amdsmi" or (kind == "auto" and spec_local and os.path.exists("/dev/kfd")):
-        return AmdSmiBackend(probe=probe, probe_period=probe_period)
+        return AmdSmiBackend(probe=probe, probe_period=probe_period, counters=counters,
+                             counters_period_ms=counters_period_ms)
     if kind == "remote" or (kind == "auto" and not spec_local):
         return RemoteBackend(transports, stream_ms=stream_ms)
     return StubBackend(stub_gpus)

@@ -5,6 +5,7 @@ Targets (all into ``native/bin`` / ``native/lib``; git-ignored, shipped with the
   * ``lib/libthsmi.so``   -- amdsmi telemetry + process attribution (ctypes)        [g++ + libamd_smi]
   * ``bin/th-smi``        -- CLI / ``--stream`` agent over the same sampler          [g++ + libamd_smi]
   * ``bin/rccl-bench``    -- RCCL/xGMI collective + direct P2P all-reduce bench      [hipcc + librccl]
+  * ``bin/th-counters``   -- device-wide HW counter sampler (rocprofiler-sdk)       [g++ + rocprofiler-sdk]
 The gfx950 kernels (incl. the th-probe kernel) are built by :mod:`..ops.build` into ``libthk.so``.
 """
 from __future__ import annotations
@@ -31,6 +32,9 @@ TARGETS = {
                                        f"-Wl,-rpath,{ROCM}/lib"]),
     "th-smi": (BIN / "th-smi", [CXX, "-O2", "-std=c++17", "-DTHSMI_MAIN", f"-I{ROCM}/include",
                                 str(HERE / "thsmi.cpp"), f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib"]),
+    "th-counters": (BIN / "th-counters", [CXX, "-O2", "-std=c++17", f"-I{ROCM}/include",
+                                          str(HERE / "th_counters.cpp"), f"-L{ROCM}/lib", "-lrocprofiler-sdk",
+                                          "-lhsa-runtime64", f"-Wl,-rpath,{ROCM}/lib"]),
     "rccl-bench": (BIN / "rccl-bench", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}",
                                         str(HERE / "rccl_bench.hip"), f"-L{ROCM}/lib", "-lrccl",
                                         f"-Wl,-rpath,{ROCM}/lib"]),

@@ -133,3 +133,30 @@ def test_daemon_with_local_amdsmi_backend(tmp_path, monkeypatch):
     finally:
         d.shutdown()
         C.set_config(None)
+
+
+def test_th_counters_device_counting():
+    """rocprofiler-sdk device counting: a busy GPU shows GRBM activity and MFMA operations."""
+    import torch
+
+    from tensorhive_fixed_amd.core.counters import derive
+    from tensorhive_fixed_amd.native.build import build_all, path_of
+
+    build_all(strict=False)
+    lst = subprocess.run([str(path_of("th-counters")), "--list"], capture_output=True, text=True, timeout=120)
+    assert lst.returncode == 0, lst.stderr[-2000:]
+    assert "GRBM_GUI_ACTIVE" in lst.stdout
+    p = subprocess.Popen([str(path_of("th-counters")), "--count", "2", "--window", "300", "--period", "400"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+    t0 = time.time()
+    while p.poll() is None and time.time() - t0 < 30:
+        for _ in range(8):
+            torch.mm(a, a)
+        torch.cuda.synchronize()
+    out, err = p.communicate(timeout=60)
+    docs = [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    assert docs and "gpus" in docs[-1], (out, err[-2000:])
+    m = derive(docs[-1]["gpus"][0], docs[-1]["window_ms"])
+    assert m["gpu_busy"]["value"] > 20.0, m
+    assert m.get("mfma_tflops", {"value": 1})["value"] > 0, m

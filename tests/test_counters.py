@@ -1,0 +1,44 @@
+"""Device-wide counter plumbing: derived metrics and the streaming reader, with a
+stand-in for the native ``th-counters`` binary (the real one is exercised in tests/gpu)."""
+import json
+import os
+import stat
+
+from tensorhive_fixed_amd.core.counters import CounterStream, derive
+
+
+def test_derive_units():
+    g = {"counters": {"GRBM_GUI_ACTIVE": 750, "GRBM_COUNT": 1000, "SQ_INSTS_VALU_MFMA_MOPS_BF16": 1e9,
+                      "TCC_EA0_RDREQ_sum": 1e9, "TCC_EA0_RDREQ_32B_sum": 0, "TCC_EA0_WRREQ_sum": 5e8,
+                      "TCC_EA0_WRREQ_64B_sum": 5e8}}
+    m = derive(g, 100.0)
+    assert m["gpu_busy"] == {"value": 75.0, "unit": "%"}
+    assert m["mfma_tflops"]["value"] == round(1e9 * 512 / 0.1 / 1e12, 1)
+    assert m["hbm_read"]["value"] == round(64e9 / 0.1 / 1e9, 1)
+    assert m["hbm_write"]["value"] == round(32e9 / 0.1 / 1e9, 1)
+    assert derive({"counters": {}}, 100.0) == {}
+
+
+def test_counter_stream_reads_lines(tmp_path):
+    line = json.dumps({"ts_ns": 1, "window_ms": 100, "gpus": [
+        {"kfd_id": 1234, "bdf": "0000:05:00.0", "counters": {"GRBM_GUI_ACTIVE": 5, "GRBM_COUNT": 10}}]})
+    fake = tmp_path / "th-counters"
+    fake.write_text(f"#!/bin/sh\necho '{line}'\nsleep 5\n")
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    cs = CounterStream(binary=str(fake))
+    try:
+        assert cs.wait_first(5)
+        assert cs.latest() == {1234: {"gpu_busy": {"value": 50.0, "unit": "%"}}}
+    finally:
+        cs.close()
+
+
+def test_counter_stream_reports_errors(tmp_path):
+    fake = tmp_path / "th-counters"
+    fake.write_text('#!/bin/sh\necho \'{"error": "no GPU agent"}\'\n')
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    cs = CounterStream(binary=str(fake))
+    try:
+        assert cs.wait_first(5) is False and cs.error == "no GPU agent"
+    finally:
+        cs.close()
