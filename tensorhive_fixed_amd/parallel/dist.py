@@ -50,16 +50,18 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # more ranks than GPUs only in tests (gloo); RCCL itself refuses two ranks on one GPU
+        idx = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     backend = None
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = "nccl" if device_type == "cuda" else "gloo"
-        kw = {"device_id": device} if device_type == "cuda" else {}
+        backend = os.environ.get("TH_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
+        kw = {"device_id": device} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     elif dist.is_initialized():
         backend = dist.get_backend()
@@ -68,7 +70,7 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
 
 def barrier(info: DistInfo) -> None:
     if info.world > 1 and dist.is_initialized():
-        if info.device.type == "cuda":
+        if info.device.type == "cuda" and info.backend == "nccl":
             dist.barrier(device_ids=[info.device.index])
         else:
             dist.barrier()

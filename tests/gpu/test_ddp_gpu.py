@@ -1,0 +1,27 @@
+"""Flat-buffer DDP on GPU tensors with several ranks (the box has one GPU: ranks share it over
+gloo; RCCL over xGMI is exercised by the driver's multi-GPU bench)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_ranks_stay_identical():
+    env = {**os.environ, "TH_DIST_BACKEND": "gloo", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "scripts/ddp_check.py"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    doc = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert doc["world"] == 2 and doc["params_identical"] and doc["n_buckets"] > 1
