@@ -66,8 +66,11 @@ def _sdpa(q, k, v):
 
 
 def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
-              causal: bool = True) -> tuple[torch.Tensor, torch.Tensor]:
-    """HIP flash attention forward on the packed layout -> (o [B*S, Hq*Dh], lse [B, Hq, S] f32)."""
+              causal: bool = True, variant: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """HIP flash attention forward on the packed layout -> (o [B*S, Hq*Dh], lse [B, Hq, S] f32).
+
+    ``variant`` (0-7, experiments only) selects a kernel variant: bit0 Q pre-scaling, bit1
+    deferred rescale, bit2 double-buffered K/V tiles; ``None`` = the built-in default."""
     row = qkv.shape[1]
     if qkv.dtype != torch.bfloat16 or not qkv.is_contiguous() or Dh != 128:
         raise ValueError("flash kernel needs contiguous bf16 packed qkv and head_dim 128")
@@ -79,8 +82,8 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
     k = q + Hq * Dh * 2
     v = k + Hkv * Dh * 2
     _lib.call("th_flash_attn_fwd", q, k, v, o.data_ptr(), lse.data_ptr(), B, S, Hq, Hkv, Dh,
-              int(causal), row, S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), 0,
-              _lib.stream_ptr(qkv.device))
+              int(causal), row, S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh),
+              0 if variant is None else 8 + (int(variant) & 7), _lib.stream_ptr(qkv.device))
     return o, lse
 
 

@@ -100,15 +100,25 @@ __device__ __forceinline__ void stage_store(char* img, const ushort8 (&r)[NP], i
 }
 
 // --------------------------------------------------------------------------------- forward
+#ifndef TH_FA_FWD_DEFAULT
+#define TH_FA_FWD_DEFAULT 0
+#endif
 constexpr int F_BM = 128, F_BN = 64;
+constexpr float F_DEFER_THR = 8.f;  // log2 units: P may reach 2^8 before O/l are rescaled
 
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Variant knobs (flags of th_flash_attn_fwd):
+//   PRESCALE  fold softmax_scale*log2(e) into Q once (no per-score multiply)
+//   DEFER     skip the O/l rescale while the running max grows by <= F_DEFER_THR (wave-uniform)
+//   DBUF      double-buffered K/V LDS tiles: ONE barrier per key tile instead of two
+template <bool PRESCALE, bool DEFER, bool DBUF>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     ushort* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hkv, long ld,
     long bs, long ldo, long bso, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * F_BN * 256];
-  char* ks = smem;
-  char* vs = smem + F_BN * 256;
+  constexpr int NBUF = DBUF ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * F_BN * 256];
   const int nqb = (S + F_BM - 1) / F_BM;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int per = Hq * B;
@@ -124,15 +134,26 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 
   bf16x8 qf[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-    qf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h)
-                        : ushort8(0));
+  for (int s = 0; s < 8; ++s) {
+    ushort8 u = q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h) : ushort8(0);
+    if (PRESCALE) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
+    }
+    qf[s] = as_bf(u);
+  }
+  const float sc = PRESCALE ? 1.f : scale_log2;
 
   const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
   const int ntiles = (kv_end + F_BN - 1) / F_BN;
   ushort8 kr[4], vr[4];
   stage_load<4>(kr, Kb, ld, 0, S, tid);
   stage_load<4>(vr, Vb, ld, 0, S, tid);
+  if (DBUF) {
+    stage_store<4>(smem, kr, tid);
+    stage_store<4>(smem + F_BN * 256, vr, tid);
+    __syncthreads();
+  }
 
   f32x16 o[4];
 #pragma unroll
@@ -140,64 +161,90 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   float m_i = -INFINITY, l_i = 0.f;
 
   for (int j = 0; j < ntiles; ++j) {
-    __syncthreads();
-    stage_store<4>(ks, kr, tid);
-    stage_store<4>(vs, vr, tid);
-    __syncthreads();
+    char* ks = smem + (DBUF ? (j & 1) : 0) * (2 * F_BN * 256);
+    char* vs = ks + F_BN * 256;
+    if (!DBUF) {
+      __syncthreads();
+      stage_store<4>(ks, kr, tid);
+      stage_store<4>(vs, vr, tid);
+      __syncthreads();
+    }
     if (j + 1 < ntiles) {
       stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
       stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
     }
     const int kbase = j * F_BN;
-    if (causal && kbase > q0 + 31) continue;  // wave-uniform: tile entirely above the diagonal
-    f32x16 sacc[2] = {f32x16(0.f), f32x16(0.f)};
+    if (!(causal && kbase > q0 + 31)) {  // wave-uniform: tile entirely above the diagonal is skipped
+      f32x16 sacc[2] = {f32x16(0.f), f32x16(0.f)};
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < 8; ++s) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) sacc[kb] = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc[kb]);
-    }
-    const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
-    float mt = -INFINITY;
+        for (int kb = 0; kb < 2; ++kb) sacc[kb] = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc[kb]);
+      }
+      const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
+      float mt = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float t = sacc[kb][r] * scale_log2;
-        if (need_mask) {
-          const int key = kbase + 32 * kb + acc_row(r, h);
-          if (key >= S || (causal && key > q)) t = -INFINITY;
+        for (int r = 0; r < 16; ++r) {
+          float t = PRESCALE ? sacc[kb][r] : sacc[kb][r] * sc;
+          if (need_mask) {
+            const int key = kbase + 32 * kb + acc_row(r, h);
+            if (key >= S || (causal && key > q)) t = -INFINITY;
+          }
+          sacc[kb][r] = t;
+          mt = fmaxf(mt, t);
         }
-        sacc[kb][r] = t;
-        mt = fmaxf(mt, t);
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      float m_use;
+      if (DEFER) {
+        if (!__all(mt - m_i <= F_DEFER_THR)) {  // some query's max moved too far: rescale now
+          const float m_new = fmaxf(m_i, mt);
+          const float mu = m_new == -INFINITY ? 0.f : m_new;
+          const float alpha = fast_exp2(m_i - mu);
+          l_i *= alpha;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) o[d] *= alpha;
+          m_i = m_new;
+        }
+        m_use = m_i == -INFINITY ? 0.f : m_i;
+      } else {
+        const float m_new = fmaxf(m_i, mt);
+        m_use = m_new == -INFINITY ? 0.f : m_new;
+        const float alpha = fast_exp2(m_i - m_use);
+        l_i *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] *= alpha;
+        m_i = m_new;
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m_i, mt);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_i - m_use);
-    float rs = 0.f;
+      float rs = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(sacc[kb][r] - m_use);
-        sacc[kb][r] = p;
-        rs += p;
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(sacc[kb][r] - m_use);
+          sacc[kb][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_i += rs;
+      bf16x8 pf[4];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        pf[2 * kb] = pack8(sacc[kb], 0);
+        pf[2 * kb + 1] = pack8(sacc[kb], 8);
       }
-    rs += __shfl_xor(rs, 32, 64);
-    l_i = l_i * alpha + rs;
-    m_i = m_new;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) o[d] *= alpha;
-    bf16x8 pf[4];
+      for (int ks4 = 0; ks4 < 4; ++ks4)
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      pf[2 * kb] = pack8(sacc[kb], 0);
-      pf[2 * kb + 1] = pack8(sacc[kb], 8);
+        for (int d = 0; d < 4; ++d) o[d] = mfma(lds_tr(vs, 16 * ks4, 32 * d, lane), pf[ks4], o[d]);
     }
-#pragma unroll
-    for (int ks4 = 0; ks4 < 4; ++ks4)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[d] = mfma(lds_tr(vs, 16 * ks4, 32 * d, lane), pf[ks4], o[d]);
+    if (DBUF && j + 1 < ntiles) {
+      char* nk = smem + ((j + 1) & 1) * (2 * F_BN * 256);
+      stage_store<4>(nk, kr, tid);
+      stage_store<4>(nk + F_BN * 256, vr, tid);
+      __syncthreads();
+    }
   }
 
   if (q < S) {
@@ -470,12 +517,25 @@ static int check_geom(int B, int S, int Hq, int Hkv, int D, long ld, long ldo) {
 extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                  int B, int S, int Hq, int Hkv, int D, int causal, long ld, long bs,
                                  long ldo, long bso, float scale, int flags, hipStream_t s) {
-  (void)flags;
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
   const long nblk = (long)((S + F_BM - 1) / F_BM) * Hq * B;
-  fa_fwd_kernel<<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                              (ushort*)o, lse, B, S, Hq, Hkv, ld, bs, ldo, bso,
-                                              scale * LOG2E, causal);
+  // flags: 0 = default variant; 1..7 = explicit (bit0 PRESCALE, bit1 DEFER, bit2 DBUF) + 8
+  const int var = flags >= 8 ? (flags & 7) : TH_FA_FWD_DEFAULT;
+#define TH_FWD(P, Dd, Db)                                                                          \
+  fa_fwd_kernel<P, Dd, Db><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,      \
+                                                         (const ushort*)v, (ushort*)o, lse, B, S,   \
+                                                         Hq, Hkv, ld, bs, ldo, bso, scale * LOG2E, causal)
+  switch (var) {
+    case 0: TH_FWD(false, false, false); break;
+    case 1: TH_FWD(true, false, false); break;
+    case 2: TH_FWD(false, true, false); break;
+    case 3: TH_FWD(true, true, false); break;
+    case 4: TH_FWD(false, false, true); break;
+    case 5: TH_FWD(true, false, true); break;
+    case 6: TH_FWD(false, true, true); break;
+    default: TH_FWD(true, true, true); break;
+  }
+#undef TH_FWD
   TH_CHECK_LAUNCH();
 }
 
