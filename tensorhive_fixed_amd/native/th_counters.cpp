@@ -209,10 +209,11 @@ std::string json_str(const std::string& s) {
 int main(int argc, char** argv) {
   bool list = false;
   int window_ms = 100, period_ms = 1000, count = 1;
-  std::vector<std::string> want = {"GRBM_GUI_ACTIVE", "GRBM_COUNT", "SQ_WAVES", "SQ_BUSY_CYCLES",
-                                   "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
-                                   "SQ_INSTS_VALU_MFMA_MOPS_F8", "TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum",
-                                   "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_WRREQ_64B_sum"};
+  // default set: the counters that read correctly in device-counting mode on gfx950
+  // (profiles/r01_counters: TCC/EA request counters and SQ_WAVES stay ~0 there)
+  std::vector<std::string> want = {"GRBM_GUI_ACTIVE", "GRBM_COUNT", "SQ_VALU_MFMA_BUSY_CYCLES",
+                                   "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F16",
+                                   "SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_INSTS_VALU_MFMA_MOPS_F32"};
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--list")) list = true;
     else if (!strcmp(argv[i], "--window") && i + 1 < argc) window_ms = atoi(argv[++i]);

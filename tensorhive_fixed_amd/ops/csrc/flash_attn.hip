@@ -101,7 +101,7 @@ __device__ __forceinline__ void stage_store(char* img, const ushort8 (&r)[NP], i
 
 // --------------------------------------------------------------------------------- forward
 #ifndef TH_FA_FWD_DEFAULT
-#define TH_FA_FWD_DEFAULT 0
+#define TH_FA_FWD_DEFAULT 3  // PRESCALE + DEFER: +8 % over 0 at B4 S4096 (scripts/flash_variants.py)
 #endif
 constexpr int F_BM = 128, F_BN = 64;
 constexpr float F_DEFER_THR = 8.f;  // log2 units: P may reach 2^8 before O/l are rescaled
