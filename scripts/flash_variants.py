@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from tensorhive_fixed_amd.ops import _lib  # noqa: E402
-from tensorhive_fixed_amd.ops.attention import attention_reference, flash_fwd  # noqa: E402
+from tensorhive_fixed_amd.ops.attention import attention_reference, flash_bwd, flash_fwd  # noqa: E402
 
 
 def main():
@@ -46,6 +46,22 @@ def main():
         dv = (o.float() - base_o).abs().max().item()
         print(json.dumps({"variant": v, "ms": round(t, 4), "tflops": round(flops / t / 1e9, 1),
                           "max_err_vs_fp32": round(err, 5), "max_diff_vs_v0": round(dv, 5)}), flush=True)
+    bwd_time(qkv, B, S, Hq, Hkv, D, flops)
+
+
+def bwd_time(qkv, B, S, Hq, Hkv, D, flops):
+    o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
+    do = torch.randn_like(o)
+    ts = []
+    for _ in range(5):
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)
+        s1.record()
+        torch.cuda.synchronize()
+        ts.append(s0.elapsed_time(s1))
+    t = sorted(ts)[2]
+    print(json.dumps({"kernel": "flash_bwd", "ms": round(t, 4), "tflops": round(2.5 * flops / t / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

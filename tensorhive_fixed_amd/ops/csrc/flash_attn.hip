@@ -80,23 +80,26 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // accumulator row (register r of lane half h) of a 32x32 MFMA tile
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// Stage `rows` x 128 bf16 rows (global, row stride ld) into registers: thread t covers row
-// 16*i + (t>>4), 16-byte chunk t&15.  Rows >= limit are zero.
+// Stage `16*NP` x 128 bf16 rows (global, row stride ld) into registers with 256 threads.
+// Thread t covers row 16*i + 4*(t>>6) + (t&3), 16-byte chunk (t>>2)&15: every 16-lane quarter of a
+// wave then writes 4 rows x 4 chunks, i.e. 16 distinct 16-byte bank slots of the LDS image --
+// conflict-free ds_write_b128 (one row per quarter-wave would be 4-way conflicted).  Rows >= limit
+// are clamped to limit-1 (finite data; the consumers mask those keys), so the loads are
+// unconditional -- no divergent branch per load.
 template <int NP>
 __device__ __forceinline__ void stage_load(ushort8 (&r)[NP], const ushort* base, long ld, int row0,
                                            int limit, int tid) {
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    const int row = row0 + 16 * i + (tid >> 4);
-    r[i] = row < limit ? *reinterpret_cast<const ushort8*>(base + (long)row * ld + ((tid & 15) << 3))
-                       : ushort8(0);
+    const int row = min(row0 + 16 * i + 4 * (tid >> 6) + (tid & 3), limit - 1);
+    r[i] = *reinterpret_cast<const ushort8*>(base + (long)row * ld + (((tid >> 2) & 15) << 3));
   }
 }
 template <int NP>
 __device__ __forceinline__ void stage_store(char* img, const ushort8 (&r)[NP], int tid) {
 #pragma unroll
   for (int i = 0; i < NP; ++i)
-    *reinterpret_cast<ushort8*>(img + img_off(16 * i + (tid >> 4), tid & 15)) = r[i];
+    *reinterpret_cast<ushort8*>(img + img_off(16 * i + 4 * (tid >> 6) + (tid & 3), (tid >> 2) & 15)) = r[i];
 }
 
 // --------------------------------------------------------------------------------- forward
@@ -181,20 +184,24 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) sacc[kb] = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc[kb]);
       }
-      const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
+      const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);  // wave-uniform
+      if (!PRESCALE) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sacc[kb] *= sc;
+      }
+      if (need_mask) {
+        const int kmax = (causal ? min(q, S - 1) : S - 1) - kbase - 4 * h;  // last visible key, tile-relative
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            sacc[kb][r] = (32 * kb + (r & 3) + 8 * (r >> 2) <= kmax) ? sacc[kb][r] : -INFINITY;
+      }
       float mt = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float t = PRESCALE ? sacc[kb][r] : sacc[kb][r] * sc;
-          if (need_mask) {
-            const int key = kbase + 32 * kb + acc_row(r, h);
-            if (key >= S || (causal && key > q)) t = -INFINITY;
-          }
-          sacc[kb][r] = t;
-          mt = fmaxf(mt, t);
-        }
+        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[kb][r]);
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       float m_use;
       if (DEFER) {
@@ -347,13 +354,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         sacc = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc);
         pacc = mfma(lds_row(vs, 32 * kb + c32, 2 * s + h), gf[s], pacc);
       }
+      const int kmax = (causal ? min(q, S - 1) : S - 1) - kbase - 32 * kb - 4 * h;  // tile-relative
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = exp2f(sacc[r] * scale_log2 - lse2);
-        if (need_mask) {
-          const int key = kbase + 32 * kb + acc_row(r, h);
-          if (key >= S || (causal && key > q)) p = 0.f;
-        }
+        float p = fast_exp2(sacc[r] * scale_log2 - lse2);
+        if (need_mask) p = ((r & 3) + 8 * (r >> 2) <= kmax) ? p : 0.f;
         sacc[r] = p * (pacc[r] - dlt);  // dS^T
       }
       const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
@@ -411,10 +416,11 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   const ushort* Kb = K + b * bs + (long)hk * HD;
   const ushort* Vb = V + b * bs + (long)hk * HD;
   {
-    // 256 rows x 16 chunks = 4096 chunks per tensor, 8 per thread (row = 32*i + tid/16)
+    // 256 rows x 16 chunks = 4096 chunks per tensor, 8 per thread; a quarter-wave covers
+    // 4 rows x 4 chunks (conflict-free ds_write_b128, see stage_load)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int row = 32 * i + (tid >> 4), ch = tid & 15;
+      const int row = 32 * i + 4 * (tid >> 6) + (tid & 3), ch = (tid >> 2) & 15;
       const bool ok = kblk0 + row < S;
       const long go = (long)(kblk0 + row) * ld + (ch << 3);
       *reinterpret_cast<ushort8*>(ks + img_off(row, ch)) = ok ? *reinterpret_cast<const ushort8*>(Kb + go) : ushort8(0);
@@ -429,8 +435,8 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   const int qt0 = causal ? kblk0 / B_BQ : 0;
   const int per_head = nqt - qt0;
   const int total = G * per_head;
-  // Q/dO tile: 32 rows x 16 chunks = 512 chunks -> one per thread per tensor
-  const int srow = tid >> 4, sch = tid & 15;
+  // Q/dO tile: 32 rows x 16 chunks = 512 chunks -> one per thread per tensor (conflict-free map)
+  const int srow = 4 * (tid >> 6) + (tid & 3), sch = (tid >> 2) & 15;
   ushort8 qr, gr;
   float lr = 0.f, dr = 0.f;
   auto prefetch = [&](int it) {
@@ -469,7 +475,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ro = (r & 3) + 8 * (r >> 2);
-      float p = exp2f(sacc[r] * scale_log2 - lsh[ro]);
+      float p = fast_exp2(sacc[r] * scale_log2 - lsh[ro]);
       if (need_mask && (key >= S || (causal && key > qbase + ro + 4 * h))) p = 0.f;
       sacc[r] = p;
       pacc[r] = p * (pacc[r] - dsh[ro]);
