@@ -69,8 +69,9 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
               causal: bool = True, variant: int | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """HIP flash attention forward on the packed layout -> (o [B*S, Hq*Dh], lse [B, Hq, S] f32).
 
-    ``variant`` (0-7, experiments only) selects a kernel variant: bit0 Q pre-scaling, bit1
-    deferred rescale, bit2 double-buffered K/V tiles; ``None`` = the built-in default."""
+    ``variant`` (0-15, experiments only) selects a kernel variant: bit0 Q pre-scaling, bit1
+    deferred rescale, bit2 double-buffered K/V tiles, bit3 KV-major block order; ``None`` = the
+    built-in default."""
     row = qkv.shape[1]
     if qkv.dtype != torch.bfloat16 or not qkv.is_contiguous() or Dh != 128:
         raise ValueError("flash kernel needs contiguous bf16 packed qkv and head_dim 128")
@@ -83,12 +84,12 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
     v = k + Hkv * Dh * 2
     _lib.call("th_flash_attn_fwd", q, k, v, o.data_ptr(), lse.data_ptr(), B, S, Hq, Hkv, Dh,
               int(causal), row, S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh),
-              0 if variant is None else 8 + (int(variant) & 7), _lib.stream_ptr(qkv.device))
+              0 if variant is None else 16 + (int(variant) & 15), _lib.stream_ptr(qkv.device))
     return o, lse
 
 
 def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, B: int,
-              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True) -> torch.Tensor:
+              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True, flags: int = 0) -> torch.Tensor:
     """HIP flash attention backward -> dqkv in the packed layout."""
     row = qkv.shape[1]
     if not do.is_contiguous():
@@ -105,7 +106,7 @@ def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.T
     dv = dk + Hkv * Dh * 2
     _lib.call("th_flash_attn_bwd", q, k, v, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
               delta.data_ptr(), dq_acc.data_ptr(), dq, dk, dv, B, S, Hq, Hkv, Dh, int(causal), row,
-              S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), 0, _lib.stream_ptr(qkv.device))
+              S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), int(flags), _lib.stream_ptr(qkv.device))
     return dqkv
 
 

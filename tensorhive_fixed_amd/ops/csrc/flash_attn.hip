@@ -102,6 +102,27 @@ __device__ __forceinline__ void stage_store(char* img, const ushort8 (&r)[NP], i
     *reinterpret_cast<ushort8*>(img + img_off(16 * i + 4 * (tid >> 6) + (tid & 3), (tid >> 2) & 15)) = r[i];
 }
 
+// Logical block -> (batch, q head, q block).  QMAJOR: q blocks heaviest-first across all heads
+// (blocks running together on an XCD touch ~16 different K/V heads: 32 MB, far beyond the XCD's
+// 4 MB L2).  KVMAJOR: all q blocks x GQA heads of ONE (batch, kv head) are contiguous, so the
+// ~64 workgroups resident on an XCD share one 2 MB K/V pair out of its L2.
+template <bool KVMAJOR>
+__device__ __forceinline__ void q_block_map(int L, int nqb, int B, int Hq, int Hkv, int& b, int& hq, int& qb) {
+  if (KVMAJOR) {
+    const int G = Hq / Hkv, per = nqb * G;
+    const int grp = L / per, r = L % per;
+    b = grp / Hkv;
+    hq = (grp % Hkv) * G + r % G;
+    qb = nqb - 1 - r / G;
+  } else {
+    const int per = Hq * B;
+    qb = nqb - 1 - L / per;
+    const int rem = L % per;
+    b = rem / Hq;
+    hq = rem % Hq;
+  }
+}
+
 // --------------------------------------------------------------------------------- forward
 #ifndef TH_FA_FWD_DEFAULT
 #define TH_FA_FWD_DEFAULT 3  // PRESCALE + DEFER: +8 % over 0 at B4 S4096 (scripts/flash_variants.py)
@@ -111,11 +132,24 @@ constexpr float F_DEFER_THR = 8.f;  // log2 units: P may reach 2^8 before O/l ar
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// lane <-> lane^32 combine with v_permlane32_swap (VALU; __shfl_xor(.,32) lowers to ds_bpermute,
+// an LDS round trip on the softmax critical path)
+__device__ __forceinline__ float half_swap_max(float x) {
+  const int xi = __builtin_bit_cast(int, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(xi, xi, false, false);
+  return fmaxf(__builtin_bit_cast(float, (int)r[0]), __builtin_bit_cast(float, (int)r[1]));
+}
+__device__ __forceinline__ float half_swap_sum(float x) {
+  const int xi = __builtin_bit_cast(int, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(xi, xi, false, false);
+  return __builtin_bit_cast(float, (int)r[0]) + __builtin_bit_cast(float, (int)r[1]);
+}
+
 // Variant knobs (flags of th_flash_attn_fwd):
 //   PRESCALE  fold softmax_scale*log2(e) into Q once (no per-score multiply)
 //   DEFER     skip the O/l rescale while the running max grows by <= F_DEFER_THR (wave-uniform)
 //   DBUF      double-buffered K/V LDS tiles: ONE barrier per key tile instead of two
-template <bool PRESCALE, bool DEFER, bool DBUF>
+template <bool PRESCALE, bool DEFER, bool DBUF, bool KVMAJOR>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     ushort* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hkv, long ld,
@@ -124,10 +158,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * F_BN * 256];
   const int nqb = (S + F_BM - 1) / F_BM;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = Hq * B;
-  const int qb = nqb - 1 - L / per;
-  const int rem = L % per;
-  const int b = rem / Hq, hq = rem % Hq, hk = hq / (Hq / Hkv);
+  int b, hq, qb;
+  q_block_map<KVMAJOR>(L, nqb, B, Hq, Hkv, b, hq, qb);
+  const int hk = hq / (Hq / Hkv);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
   const int q0 = qb * F_BM + w * 32;
   const int q = q0 + c32;
@@ -179,10 +212,22 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const int kbase = j * F_BN;
     if (!(causal && kbase > q0 + 31)) {  // wave-uniform: tile entirely above the diagonal is skipped
       f32x16 sacc[2] = {f32x16(0.f), f32x16(0.f)};
+      {  // K-row operands are read one k-step ahead of the MFMAs that use them
+        bf16x8 a0 = lds_row(ks, c32, h), a1 = lds_row(ks, 32 + c32, h);
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) sacc[kb] = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc[kb]);
+        for (int s = 0; s < 8; ++s) {
+          bf16x8 n0 = a0, n1 = a1;
+          if (s < 7) {
+            n0 = lds_row(ks, c32, 2 * s + 2 + h);
+            n1 = lds_row(ks, 32 + c32, 2 * s + 2 + h);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
+          sacc[0] = mfma(a0, qf[s], sacc[0]);
+          sacc[1] = mfma(a1, qf[s], sacc[1]);
+          __builtin_amdgcn_sched_barrier(0);
+          a0 = n0;
+          a1 = n1;
+        }
       }
       const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);  // wave-uniform
       if (!PRESCALE) {
@@ -202,7 +247,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[kb][r]);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      mt = half_swap_max(mt);
       float m_use;
       if (DEFER) {
         if (!__all(mt - m_i <= F_DEFER_THR)) {  // some query's max moved too far: rescale now
@@ -233,18 +278,30 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
           sacc[kb][r] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 32, 64);
-      l_i += rs;
+      l_i += half_swap_sum(rs);
       bf16x8 pf[4];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         pf[2 * kb] = pack8(sacc[kb], 0);
         pf[2 * kb + 1] = pack8(sacc[kb], 8);
       }
+      {  // V^T operands read one k-step ahead
+        bf16x8 vt[4];
 #pragma unroll
-      for (int ks4 = 0; ks4 < 4; ++ks4)
+        for (int d = 0; d < 4; ++d) vt[d] = lds_tr(vs, 0, 32 * d, lane);
 #pragma unroll
-        for (int d = 0; d < 4; ++d) o[d] = mfma(lds_tr(vs, 16 * ks4, 32 * d, lane), pf[ks4], o[d]);
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          bf16x8 nx[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) nx[d] = ks4 < 3 ? lds_tr(vs, 16 * ks4 + 16, 32 * d, lane) : vt[d];
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int d = 0; d < 4; ++d) o[d] = mfma(vt[d], pf[ks4], o[d]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int d = 0; d < 4; ++d) vt[d] = nx[d];
+        }
+      }
     }
     if (DBUF && j + 1 < ntiles) {
       char* nk = smem + ((j + 1) & 1) * (2 * F_BN * 256);
@@ -293,6 +350,7 @@ __global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict_
 }
 
 // ------------------------------------------------------------------------------- dQ kernel
+template <bool KVMAJOR>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
@@ -303,10 +361,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   char* vs = smem + F_BN * 256;
   const int nqb = (S + F_BM - 1) / F_BM;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = Hq * B;
-  const int qb = nqb - 1 - L / per;
-  const int rem = L % per;
-  const int b = rem / Hq, hq = rem % Hq, hk = hq / (Hq / Hkv);
+  int b, hq, qb;
+  q_block_map<KVMAJOR>(L, nqb, B, Hq, Hkv, b, hq, qb);
+  const int hk = hq / (Hq / Hkv);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
   const int q0 = qb * F_BM + w * 32;
   const int q = q0 + c32;
@@ -525,21 +582,27 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
                                  long ldo, long bso, float scale, int flags, hipStream_t s) {
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
   const long nblk = (long)((S + F_BM - 1) / F_BM) * Hq * B;
-  // flags: 0 = default variant; 1..7 = explicit (bit0 PRESCALE, bit1 DEFER, bit2 DBUF) + 8
-  const int var = flags >= 8 ? (flags & 7) : TH_FA_FWD_DEFAULT;
-#define TH_FWD(P, Dd, Db)                                                                          \
-  fa_fwd_kernel<P, Dd, Db><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,      \
-                                                         (const ushort*)v, (ushort*)o, lse, B, S,   \
-                                                         Hq, Hkv, ld, bs, ldo, bso, scale * LOG2E, causal)
+  // flags: 0 = default variant; 16 + v = explicit v (bit0 PRESCALE, bit1 DEFER, bit2 DBUF,
+  // bit3 KVMAJOR block order)
+  const int var = flags >= 16 ? (flags & 15) : TH_FA_FWD_DEFAULT;
+#define TH_FWD(P, Dd, Db, Km)                                                                      \
+  fa_fwd_kernel<P, Dd, Db, Km><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,  \
+                                                             (const ushort*)v, (ushort*)o, lse, B,  \
+                                                             S, Hq, Hkv, ld, bs, ldo, bso,          \
+                                                             scale * LOG2E, causal)
   switch (var) {
-    case 0: TH_FWD(false, false, false); break;
-    case 1: TH_FWD(true, false, false); break;
-    case 2: TH_FWD(false, true, false); break;
-    case 3: TH_FWD(true, true, false); break;
-    case 4: TH_FWD(false, false, true); break;
-    case 5: TH_FWD(true, false, true); break;
-    case 6: TH_FWD(false, true, true); break;
-    default: TH_FWD(true, true, true); break;
+    case 0: TH_FWD(false, false, false, false); break;
+    case 1: TH_FWD(true, false, false, false); break;
+    case 2: TH_FWD(false, true, false, false); break;
+    case 3: TH_FWD(true, true, false, false); break;
+    case 4: TH_FWD(false, false, true, false); break;
+    case 5: TH_FWD(true, false, true, false); break;
+    case 6: TH_FWD(false, true, true, false); break;
+    case 7: TH_FWD(true, true, true, false); break;
+    case 8: TH_FWD(false, false, false, true); break;
+    case 11: TH_FWD(true, true, false, true); break;
+    case 15: TH_FWD(true, true, true, true); break;
+    default: TH_FWD(true, true, false, true); break;
   }
 #undef TH_FWD
   TH_CHECK_LAUNCH();
@@ -550,16 +613,21 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
                                  void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv, int D,
                                  int causal, long ld, long bs, long ldo, long bso, float scale,
                                  int flags, hipStream_t s) {
-  (void)flags;
   (void)dq_acc;
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
   const long rows = (long)B * S * Hq;
   fa_delta_kernel<<<(unsigned)((rows + 15) / 16), 256, 0, s>>>((const ushort*)o, (const ushort*)dout,
                                                                delta, B, S, Hq, ldo, bso);
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
-  fa_bwd_dq_kernel<<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                (const ushort*)dout, lse, delta, (ushort*)dq, B, S, Hq,
-                                                Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+  // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map)
+  if (flags & 1)
+    fa_bwd_dq_kernel<false><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                         (const ushort*)dout, lse, delta, (ushort*)dq, B, S,
+                                                         Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+  else
+    fa_bwd_dq_kernel<true><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                        (const ushort*)dout, lse, delta, (ushort*)dq, B, S,
+                                                        Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
   const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;
   static bool attr_set = false;
   if (!attr_set) {
