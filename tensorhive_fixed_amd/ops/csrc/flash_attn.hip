@@ -125,7 +125,7 @@ __device__ __forceinline__ void q_block_map(int L, int nqb, int B, int Hq, int H
 
 // --------------------------------------------------------------------------------- forward
 #ifndef TH_FA_FWD_DEFAULT
-#define TH_FA_FWD_DEFAULT 3  // PRESCALE + DEFER: +8 % over 0 at B4 S4096 (scripts/flash_variants.py)
+#define TH_FA_FWD_DEFAULT 11  // PRESCALE + DEFER + KVMAJOR: 747 vs 447 TFLOP/s for 0 (B4 S4096, profiles/r01_flash)
 #endif
 constexpr int F_BM = 128, F_BN = 64;
 constexpr float F_DEFER_THR = 8.f;  // log2 units: P may reach 2^8 before O/l are rescaled
@@ -446,6 +446,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 // hoisting them would cost 64 VGPRs and drop the kernel to one wave per SIMD).
 constexpr int B_BK = 256, B_BQ = 32, B_THREADS = 512;
 
+template <bool KVMAJOR>
 __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
@@ -461,10 +462,19 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   float* ds = ls + B_BQ;
   const int nkb = (S + B_BK - 1) / B_BK;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = Hkv * B;
-  const int kblk = causal ? L / per : nkb - 1 - L / per;  // causal: low key blocks are heaviest
-  const int rem = L % per;
-  const int b = rem / Hkv, hk = rem % Hkv;
+  int b, hk, kblk;
+  if (KVMAJOR) {  // the key blocks of one (batch, kv head) together: they stream the same Q/dO
+    const int grp = L / nkb, r = L % nkb;
+    b = grp / Hkv;
+    hk = grp % Hkv;
+    kblk = causal ? r : nkb - 1 - r;  // causal: low key blocks are heaviest
+  } else {
+    const int per = Hkv * B;
+    kblk = causal ? L / per : nkb - 1 - L / per;
+    const int rem = L % per;
+    b = rem / Hkv;
+    hk = rem % Hkv;
+  }
   const int G = Hq / Hkv;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
   const int kblk0 = kblk * B_BK;
@@ -631,12 +641,18 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dkv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, B_LDS);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkv_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, B_LDS);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkv_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, B_LDS);
     attr_set = true;
   }
-  fa_bwd_dkv_kernel<<<(unsigned)nk, B_THREADS, B_LDS, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                 (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
-                                                 B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
-                                                 causal);
+  // flags bit1: the old (kv-block-major) order for dK/dV (default: KV-head-major)
+  if (flags & 2)
+    fa_bwd_dkv_kernel<false><<<(unsigned)nk, B_THREADS, B_LDS, s>>>(
+        (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
+        (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+  else
+    fa_bwd_dkv_kernel<true><<<(unsigned)nk, B_THREADS, B_LDS, s>>>(
+        (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
+        (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
   TH_CHECK_LAUNCH();
 }
