@@ -33,6 +33,7 @@ def main() -> int:
     ap.add_argument("--seq-len", type=int, default=int(os.environ.get("TH_BENCH_SEQ", "4096")))
     ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("TH_BENCH_MB", "4")))
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("TH_BENCH_BUCKET_MB", "256")))
+    ap.add_argument("--grad-accum", type=int, default=int(os.environ.get("TH_BENCH_ACCUM", "1")))
     args = ap.parse_args()
 
     import torch
@@ -49,7 +50,7 @@ def main() -> int:
     if info.world != args.gpus and info.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {info.world}", file=sys.stderr)
     cfg = LlamaConfig.named(args.model)
-    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, 1, bucket_mb=args.bucket_mb)
+    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb)
     res = run_timed(tr, args.steps, args.warmup)
     n = info.world
     flops = cfg.flops_per_token(args.seq_len) * res["tokens_per_sec"]
@@ -68,9 +69,11 @@ def main() -> int:
         "data": "synthetic",
         "config": {
             "model": "Llama-3-8B" if args.model in ("llama3-8b", "llama3_8b") else args.model,
-            "global_batch": args.micro_batch * n,
+            "global_batch": args.micro_batch * args.grad_accum * n,
+            "micro_batch": args.micro_batch,
+            "grad_accum": args.grad_accum,
             "seq_len": args.seq_len,
-            "tokens_per_gpu_per_step": args.micro_batch * args.seq_len,
+            "tokens_per_gpu_per_step": args.micro_batch * args.grad_accum * args.seq_len,
             "parallelism": f"dp{n}",
             "optimizer": "AdamW (fp32 master, fused flat kernel, clip 1.0)",
             "attention": attention_backend(),

@@ -451,7 +451,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
-    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal, int young_prio) {
   // K image 64 KB | V image 64 KB | Q tile 8 KB | dO tile 8 KB | lse 128 B | delta 128 B
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ks = smem;
@@ -521,6 +521,9 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   };
   if (total > 0) prefetch(0);
   int krow = 32 * w + c32;
+  // static priority for the second-dispatched half (waves 4-7): it otherwise loses VALU
+  // arbitration to its SIMD partner on every segment (guide T5, static form)
+  if (young_prio && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int it = 0; it < total; ++it) {
     __syncthreads();
     *reinterpret_cast<ushort8*>(qs + img_off(srow, sch)) = qr;
@@ -537,15 +540,19 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
 #pragma unroll
     for (int s = 0; s < 8; ++s) pacc = mfma(lds_row(gs, c32, 2 * s + h), lds_row(vs, krow, 2 * s + h), pacc);
     const bool need_mask = (causal && qbase < k0 + 31) || key >= S;
-    const float* lsh = ls + 4 * h;  // one base per lane; the row offsets below are immediates
-    const float* dsh = ds + 4 * h;
+    // lse / delta of the accumulator rows (4h + (r&3) + 8(r>>2)): four 16-byte reads each
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ro = (r & 3) + 8 * (r >> 2);
-      float p = fast_exp2(sacc[r] * scale_log2 - lsh[ro]);
-      if (need_mask && (key >= S || (causal && key > qbase + ro + 4 * h))) p = 0.f;
-      sacc[r] = p;
-      pacc[r] = p * (pacc[r] - dsh[ro]);
+    for (int g = 0; g < 4; ++g) {
+      const float4v lv = *reinterpret_cast<const float4v*>(ls + 4 * h + 8 * g);
+      const float4v dv4 = *reinterpret_cast<const float4v*>(ds + 4 * h + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e, ro = e + 8 * g;
+        float p = fast_exp2(sacc[r] * scale_log2 - lv[e]);
+        if (need_mask && (key >= S || (causal && key > qbase + ro + 4 * h))) p = 0.f;
+        sacc[r] = p;
+        pacc[r] = p * (pacc[r] - dv4[e]);
+      }
     }
     const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
     const bf16x8 s0 = pack8(pacc, 0), s1 = pack8(pacc, 8);
@@ -649,10 +656,10 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   if (flags & 2)
     fa_bwd_dkv_kernel<false><<<(unsigned)nk, B_THREADS, B_LDS, s>>>(
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
-        (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+        (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, !(flags & 4));
   else
     fa_bwd_dkv_kernel<true><<<(unsigned)nk, B_THREADS, B_LDS, s>>>(
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
-        (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+        (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, !(flags & 4));
   TH_CHECK_LAUNCH();
 }
