@@ -139,8 +139,9 @@ def poll_latency(requests: int = 1000, nodes: int = 8, gpus: int = 8, warmup: in
         return {"metric": "dashboard_poll_latency", "nodes": nodes, "gpus_per_node": gpus, "results": out}
 
 
-def launch_latency(trials: int = 5, command: str = "sleep 2") -> dict:
-    """Enqueue -> task process running, through the real scheduler thread and th-run."""
+def launch_latency(trials: int = 5, command: str = "echo started; sleep 2") -> dict:
+    """Enqueue -> task process running (scheduler launch log) and -> first line in the task's log
+    (BASELINE.md §2 definition), through the real scheduler thread and th-run."""
     from .controllers import task as task_ctl
     from .core.daemon import Daemon
     from .core.services import JobSchedulingService
@@ -168,7 +169,7 @@ def launch_latency(trials: int = 5, command: str = "sleep 2") -> dict:
         seg = CommandSegment(name="HIP_VISIBLE_DEVICES", _segment_type=SegmentType.env_variable)
         seg.save()
         sched.start()
-        lat = []
+        lat, first_line = [], []
         try:
             for i in range(trials):
                 job = Job(name=f"bench-{i}", description="", user_id=u.id)
@@ -189,13 +190,23 @@ def launch_latency(trials: int = 5, command: str = "sleep 2") -> dict:
                     raise TimeoutError(f"job {job.id} was not launched within 30 s")
                 ts = dict(sched.launch_log)[job.id]
                 lat.append((ts - t0) * 1e3)
+                from .core import task_nursery
                 from .database import db_session
+
+                tid = job.tasks[0].id
+                while time.time() < deadline:
+                    try:
+                        lines, _ = task_nursery.fetch_log("localhost", u.username, tid)
+                    except FileNotFoundError:
+                        lines = []
+                    if lines:
+                        first_line.append((time.time() - t0) * 1e3)
+                        break
+                    time.sleep(0.002)
 
                 db_session.expire_all()
                 t = Task.get(t.id)
                 assert t.status is TaskStatus.running and t.pid, t.as_dict()
-                from .core import task_nursery
-
                 task_nursery.terminate(t.pid, "localhost", u.username, gracefully=False)
                 task_ctl.synchronize(t.id)
                 job = Job.get(job.id)
@@ -204,7 +215,70 @@ def launch_latency(trials: int = 5, command: str = "sleep 2") -> dict:
             daemon.shutdown()
         return {"metric": "queued_job_launch_latency", "trials": trials,
                 "p50_ms": round(_pct(lat, 0.5), 2), "max_ms": round(max(lat), 2),
+                "first_log_line_p50_ms": round(_pct(first_line, 0.5), 2) if first_line else None,
                 "reference_ms": 30000.0 / 2, "note": "reference polls every 30 s -> 15 s mean wait"}
+
+
+def scheduled_training(gpus: int = 1, steps: int = 10, warmup: int = 2, micro_batch: int = 8,
+                       model: str = "llama3-8b", timeout_s: float = 900.0) -> dict:
+    """BASELINE config 3/4: the Llama-3 DDP payload launched BY THE JOB QUEUE -- torchrun template,
+    HIP_VISIBLE_DEVICES from the GPUs' HIP indices, real amdsmi telemetry for the free-GPU check --
+    and its tokens/s read back from the task log (``[th-train]`` lines)."""
+    import re
+
+    from .core import task_nursery
+    from .core.daemon import Daemon
+    from .core.launcher import torchrun_task
+    from .core.services import JobSchedulingService
+    from .core.telemetry import AmdSmiBackend
+    from .controllers import task as task_ctl
+    from .models.orm import Job, Restriction
+    from .native.build import build_all
+    from .utils import dates
+
+    me = getpass.getuser()
+    if me == "root":
+        return {"metric": "scheduled_training", "skipped": "run as an ordinary user"}
+    build_all(strict=False)
+    with sandbox({"localhost": "local"}, job_interval=3600.0) as (cfg, _d):
+        smi = AmdSmiBackend()
+        daemon = Daemon(cfg, backends={"localhost": smi}, init_key=False, test_ssh=False)
+        daemon.infrastructure.publish("localhost", smi.sample("localhost"))
+        sched = JobSchedulingService(3600.0, 5, 10)
+        daemon.add_service(sched)
+        u = _admin(me)
+        r = Restriction(name="all", starts_at=dates.utcnow(), is_global=True)
+        r.save()
+        r.apply_to_user(u)
+        form = torchrun_task("localhost", list(range(gpus)), "127.0.0.1", 29533,
+                             script_args=[("--steps", str(steps)), ("--warmup", str(warmup)),
+                                          ("--micro-batch", str(micro_batch)), ("--model", model)])
+        job = Job(name="llama3-ddp", description="scheduled training", user_id=u.id)
+        job.save()
+        content, status = task_ctl.business_create(form, job.id)
+        assert status == 201, content
+        tid = content["task"]["id"]
+        job = Job.get(job.id)
+        job.enqueue()
+        sched.start()
+        t0 = time.time()
+        daemon.wake("enqueue")
+        rates, done, lines = [], False, []
+        try:
+            while time.time() - t0 < timeout_s and not done:
+                time.sleep(1.0)
+                try:
+                    lines, _ = task_nursery.fetch_log("localhost", me, tid)
+                except FileNotFoundError:
+                    continue
+                rates = [float(m.group(1)) for l in lines for m in [re.search(r"tokens/s=([0-9.]+)", l)] if m]
+                done = any('"event": "done"' in l for l in lines)
+        finally:
+            daemon.shutdown()
+        steady = rates[1:] or rates
+        return {"metric": "scheduled_llama3_ddp_tokens_per_sec", "gpus": gpus, "micro_batch": micro_batch,
+                "steps_logged": len(rates), "tokens_per_sec": round(statistics.fmean(steady), 1) if steady else None,
+                "completed": done, "wall_s": round(time.time() - t0, 1), "log_tail": lines[-3:]}
 
 
 def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3) -> dict:

@@ -6,7 +6,7 @@
     tensorhive key                                              print the authorized_keys line
     tensorhive create user [-m]                                 account prompt (repeat with -m)
     tensorhive doctor                                           ROCm / amdsmi / RCCL / xGMI checks (new)
-    tensorhive bench poll|launch|train                          N08 benchmark harnesses (new)
+    tensorhive bench poll|launch|train|scheduled                N08 benchmark harnesses (new)
     tensorhive profile --task ID                                rocprofv3 wrapper line for a task (new)
 
 Fixes vs. the reference: ``init`` is a function the main command can call (the reference invoked
@@ -207,7 +207,7 @@ def doctor():
 
 
 @main.command()
-@click.argument("what", type=click.Choice(["poll", "launch", "train"]))
+@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled"]))
 @click.option("--requests", default=1000)
 @click.option("--gpus", default=1)
 def bench(what, requests, gpus):
@@ -218,6 +218,8 @@ def bench(what, requests, gpus):
         click.echo(json.dumps(benchmarks.poll_latency(requests)))
     elif what == "launch":
         click.echo(json.dumps(benchmarks.launch_latency()))
+    elif what == "scheduled":
+        click.echo(json.dumps(benchmarks.scheduled_training(gpus)))
     else:
         click.echo(json.dumps(benchmarks.train_throughput(gpus)))
 
