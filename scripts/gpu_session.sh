@@ -27,6 +27,7 @@ for s in ${TH_STEPS:-tests bench}; do
     native) step native_tests 600 python -m pytest tests/gpu/test_native_gpu.py -x -q ;;
     doctor) step doctor 300 python -m tensorhive_fixed_amd doctor ;;
     daemon_bench) step daemon_bench 300 python -c "import json; from tensorhive_fixed_amd import benchmarks as b; print(json.dumps(b.poll_latency(1000))); print(json.dumps(b.launch_latency(5)))" ;;
+    scheduled) step scheduled 900 python -c "import json; from tensorhive_fixed_amd import benchmarks as b; print(json.dumps(b.scheduled_training(1, steps=8)))" ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
   esac
 done
