@@ -195,6 +195,7 @@ EXTRA_OPERATIONS: list[Op] = [
     Op("GET", "/nodes/topology", "nodes.get_topology", "jwt", tag="nodes"),                       # new
     Op("GET", "/metrics/internal", "nodes.get_internal_metrics", "admin", tag="nodes"),            # new
     Op("GET", "/jobs/templates", "job.get_templates", "jwt", tag="jobs"),                         # new
+    Op("GET", "/metrics/prometheus", "nodes.get_prometheus", None, tag="nodes"),                  # new
 ]
 
 COMPAT_OPERATION_COUNT = 66

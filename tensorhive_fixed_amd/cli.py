@@ -15,6 +15,7 @@ instead of ``/home/tensorhive/.logs``; config files are created explicitly, not 
 """
 from __future__ import annotations
 
+import io
 import json
 import logging
 import os
@@ -102,6 +103,12 @@ def do_init() -> None:
 @click.option("--json-logs", is_flag=True)
 @click.pass_context
 def main(ctx, version, log_level, log_dir, config_dir, json_logs):
+    import faulthandler
+
+    try:  # tracebacks of every thread on SIGSEGV/SIGABRT (daemon threads, native libs)
+        faulthandler.enable(file=sys.__stderr__)
+    except (AttributeError, ValueError, OSError, io.UnsupportedOperation):
+        pass  # no real stderr (embedded / test runner)
     if version:
         click.echo(__version__)
         return

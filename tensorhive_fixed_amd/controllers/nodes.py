@@ -141,6 +141,46 @@ def get_topology():
     return d.topology(), 200
 
 
+def _prom_escape(v) -> str:
+    return str(v).replace("\\", "\\\\").replace('"', '\\"')
+
+
+def get_prometheus():
+    """Prometheus text exposition of the latest snapshot: numeric GPU/CPU metrics per host and GPU,
+    snapshot age per host, service loop timings.  No user names or process lists (unauthenticated
+    scrape target)."""
+    import time
+
+    d = daemon()
+    lines = ["# TYPE tensorhive_gpu_metric gauge", "# TYPE tensorhive_sample_age_seconds gauge"]
+    if d is not None:
+        snap = d.infrastructure.snapshot()
+        now = time.time()
+        for host, entry in sorted(snap.data.items()):
+            h = _prom_escape(host)
+            if host in snap.sampled_at:
+                lines.append(f'tensorhive_sample_age_seconds{{host="{h}"}} {now - snap.sampled_at[host]:.3f}')
+            for uuid, g in sorted(((entry or {}).get("GPU") or {}).items()):
+                for name, m in sorted((g.get("metrics") or {}).items()):
+                    v = (m or {}).get("value")
+                    if isinstance(v, (int, float)):
+                        lines.append(f'tensorhive_gpu_metric{{host="{h}",gpu="{g.get("index")}",uuid="{uuid}",'
+                                     f'metric="{_prom_escape(name)}",unit="{_prom_escape(m.get("unit", ""))}"}} {v}')
+                lines.append(f'tensorhive_gpu_processes{{host="{h}",gpu="{g.get("index")}",uuid="{uuid}"}} '
+                             f'{len(g.get("processes") or [])}')
+            for cpu in ((entry or {}).get("CPU") or {}).values():
+                for name, m in sorted((cpu.get("metrics") or {}).items()):
+                    v = (m or {}).get("value")
+                    if isinstance(v, (int, float)):
+                        lines.append(f'tensorhive_cpu_metric{{host="{h}",metric="{_prom_escape(name)}"}} {v}')
+        for svc, st in d.service_stats().items():
+            for k in ("p50_ms", "p99_ms"):
+                if isinstance(st.get(k), (int, float)):
+                    lines.append(f'tensorhive_service_loop_ms{{service="{svc}",quantile="{k[:3]}"}} {st[k]}')
+            lines.append(f'tensorhive_service_ticks_total{{service="{svc}"}} {st.get("ticks", 0)}')
+    return Response("\n".join(lines) + "\n", status=200, mimetype="text/plain; version=0.0.4")
+
+
 def get_internal_metrics():
     """Service loop timings and API latency percentiles (observability, new)."""
     from flask import current_app

@@ -34,6 +34,7 @@ TEMPLATES = {
         "params": [{"name": "--nnodes=", "value": "1"}, {"name": "--nproc_per_node=", "value": "<#GPUs>"},
                    {"name": "--rdzv_backend=", "value": "c10d"},
                    {"name": "--rdzv_endpoint=", "value": "<host>:29500"},
+                   {"name": "--max-restarts=", "value": "0"},
                    {"name": "-m", "value": "tensorhive_fixed_amd.workloads.llama3_ddp"}],
     },
     "pytorch_tcp": {

@@ -41,6 +41,24 @@ TARGETS = {
 }
 
 
+# ASan + UBSan builds of the host tools (``th-run-asan``, ``th-smi-asan``): built on demand by the
+# sanitizer tests, never shipped.  Host code only -- GPU sanitizers are not used on this pool.
+SANITIZE = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+for _n in ("th-run", "th-smi"):
+    _out, _cmd = TARGETS[_n]
+    TARGETS[_n + "-asan"] = (_out.with_name(_out.name + "-asan"),
+                             [_cmd[0]] + SANITIZE + [c for c in _cmd[1:] if c not in ("-O2", "-O3")])
+SANITIZED = {n for n in TARGETS if n.endswith("-asan")}
+
+
+def sanitizer_env(report_dir: str) -> dict:
+    """Environment for running a ``*-asan`` binary: reports go to files under ``report_dir`` (one per
+    process, so forked monitors are covered too) and any finding makes the process fail."""
+    return {"ASAN_OPTIONS": f"log_path={report_dir}/asan:detect_leaks=1:abort_on_error=0:exitcode=99:"
+                            "verify_asan_link_order=0:detect_stack_use_after_return=1",
+            "UBSAN_OPTIONS": f"log_path={report_dir}/ubsan:halt_on_error=1:print_stacktrace=1"}
+
+
 def path_of(name: str) -> Path:
     return TARGETS[name][0]
 
@@ -63,7 +81,7 @@ def _build_one(name: str, force: bool) -> tuple[str, str | None]:
 
 def build_all(force: bool = False, strict: bool = True) -> dict[str, str | None]:
     with cf.ThreadPoolExecutor(max_workers=4) as ex:
-        results = dict(ex.map(lambda n: _build_one(n, force), TARGETS))
+        results = dict(ex.map(lambda n: _build_one(n, force), [n for n in TARGETS if n not in SANITIZED]))
     errs = {k: v for k, v in results.items() if v}
     for k, v in errs.items():
         print(f"[native] {k}: FAILED\n{v}", file=sys.stderr)
@@ -87,4 +105,4 @@ def th_run_binary() -> str:
 
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv)
-    print("[native] built:", ", ".join(str(v[0]) for v in TARGETS.values()))
+    print("[native] built:", ", ".join(str(v[0]) for n, v in TARGETS.items() if n not in SANITIZED))

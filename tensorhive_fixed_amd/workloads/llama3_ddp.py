@@ -31,11 +31,34 @@ class SyntheticTokens:
         self.vocab, self.batch, self.seq, self.device = vocab, batch, seq, device
         self.gen = torch.Generator(device=device)
         self.gen.manual_seed(seed + 7919 * rank)
+        self.drawn = 0  # batches handed out: a resume replays this many draws on every rank
+
+    def skip(self, n: int) -> None:
+        for _ in range(n):
+            self.next()
 
     def next(self) -> tuple[torch.Tensor, torch.Tensor]:
+        self.drawn += 1
         buf = torch.randint(0, self.vocab, (self.batch, self.seq + 1), device=self.device,
                             generator=self.gen)
         return buf[:, :-1], buf[:, 1:]
+
+
+class _Range:
+    """roctx range (``TH_ROCTX=1``): shows steps / fwd / bwd / optimizer on rocprofv3 --marker-trace."""
+
+    enabled = os.environ.get("TH_ROCTX") == "1"
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        if self.enabled:
+            torch.cuda.nvtx.range_push(self.name)  # roctx on ROCm builds
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            torch.cuda.nvtx.range_pop()
 
 
 class Trainer:
@@ -54,16 +77,48 @@ class Trainer:
     def step(self) -> torch.Tensor:
         n_valid = self.micro_batch * self.seq_len
         loss_acc = None
-        for mb in range(self.grad_accum):
-            tokens, targets = self.data.next()
-            self.store.begin_microbatch(accumulate=mb > 0, sync=mb == self.grad_accum - 1)
-            loss = self.model(tokens, targets, n_valid=n_valid * self.grad_accum)
-            loss.backward()
-            loss_acc = loss.detach() if loss_acc is None else loss_acc + loss.detach()
-        self.store.finish_grad_sync()
-        self.opt.step()
+        with _Range("train_step"):
+            for mb in range(self.grad_accum):
+                tokens, targets = self.data.next()
+                self.store.begin_microbatch(accumulate=mb > 0, sync=mb == self.grad_accum - 1)
+                with _Range("forward"):
+                    loss = self.model(tokens, targets, n_valid=n_valid * self.grad_accum)
+                with _Range("backward"):
+                    loss.backward()
+                loss_acc = loss.detach() if loss_acc is None else loss_acc + loss.detach()
+            with _Range("grad_sync+adamw"):
+                self.store.finish_grad_sync()
+                self.opt.step()
         self.last_loss = loss_acc
         return loss_acc
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state(self) -> dict:
+        """Everything a bit-exact resume needs: flat params, f32 master / moments, step, data RNG."""
+        return {"param_buf": self.store.param_buf, "master": self.opt.master, "exp_avg": self.opt.exp_avg,
+                "exp_avg_sq": self.opt.exp_avg_sq, "step": torch.tensor(self.opt.step_count),
+                "data_drawn": torch.tensor(self.data.drawn), "names": "\n".join(self.store.names)}
+
+    def save(self, path: str) -> None:
+        """Rank 0 writes (replicas are identical under DDP); atomic rename."""
+        if self.info.rank != 0:
+            return
+        tmp = path + ".tmp"
+        torch.save({k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in self.state().items()}, tmp)
+        os.replace(tmp, path)
+
+    def load(self, path: str) -> None:
+        st = torch.load(path, map_location="cpu", weights_only=True)
+        if st["names"] != "\n".join(self.store.names):
+            raise ValueError("checkpoint does not match this model's parameter layout")
+        with torch.no_grad():
+            self.store.param_buf.copy_(st["param_buf"])
+            self.opt.master.copy_(st["master"])
+            self.opt.exp_avg.copy_(st["exp_avg"])
+            self.opt.exp_avg_sq.copy_(st["exp_avg_sq"])
+        self.opt.step_count = int(st["step"])
+        # every rank has its own data stream: replay the same number of draws on each
+        self.data.skip(int(st["data_drawn"]) - self.data.drawn)
 
 
 def sync_device(info: DistInfo) -> None:
@@ -91,6 +146,12 @@ def run_timed(trainer: Trainer, steps: int, warmup: int) -> dict:
             "loss": loss}
 
 
+def _maybe_save(tr: Trainer, ckpt: str | None, args) -> None:
+    if ckpt and args.ckpt_every and tr.opt.step_count % args.ckpt_every == 0:
+        os.makedirs(os.path.dirname(ckpt), exist_ok=True)
+        tr.save(ckpt)
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description="Llama-3 bf16 DDP training on MI355X (synthetic data)")
     ap.add_argument("--model", default="llama3-8b")
@@ -101,16 +162,29 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--ckpt-dir", default=None, help="write <dir>/ckpt.pt every --ckpt-every steps (rank 0)")
+    ap.add_argument("--ckpt-every", type=int, default=0)
+    ap.add_argument("--resume", action="store_true", help="continue from <ckpt-dir>/ckpt.pt if present")
     args = ap.parse_args(argv)
     info = init_distributed()
     cfg = LlamaConfig.named(args.model)
     tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb)
-    for _ in range(args.warmup):
+    ckpt = os.path.join(args.ckpt_dir, "ckpt.pt") if args.ckpt_dir else None
+    if ckpt and args.resume and os.path.exists(ckpt):
+        tr.load(ckpt)
+        if info.is_main:
+            print(json.dumps({"event": "resumed", "step": tr.opt.step_count}), flush=True)
+    # warm-up steps are real optimizer steps (excluded from the timing only); a resumed run continues
+    # the same global step count up to warmup + steps
+    total = args.warmup + args.steps
+    while tr.opt.step_count < min(args.warmup, total):
         tr.step()
+        _maybe_save(tr, ckpt, args)
     sync_device(info)
     t_last = time.perf_counter()
-    for s in range(1, args.steps + 1):
+    while tr.opt.step_count < total:
         tr.step()
+        s = tr.opt.step_count - args.warmup
         if s % args.log_every == 0:
             sync_device(info)
             now = time.perf_counter()
@@ -120,8 +194,10 @@ def main(argv: list[str] | None = None) -> int:
             if info.is_main:
                 print(f"[th-train] step={s} loss={float(tr.last_loss):.4f} tokens/s={tps:.1f} "
                       f"world={info.world}", flush=True)
+        _maybe_save(tr, ckpt, args)
     if info.is_main:
-        print(json.dumps({"event": "done", "steps": args.steps}), flush=True)
+        print(json.dumps({"event": "done", "steps": tr.opt.step_count,
+                          "loss": round(float(tr.last_loss), 6) if tr.last_loss is not None else None}), flush=True)
     shutdown()
     return 0
 

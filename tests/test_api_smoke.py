@@ -43,3 +43,20 @@ def test_reservation_flow(client, new_user, auth_headers, resource1, permissive_
     assert data["reservation"]["start"].endswith("+00:00")
     st, data = api(client, "post", "/reservations", auth_headers(new_user), body)
     assert st == 422  # overlap
+
+
+def test_prometheus_exposition(client, daemon):
+    daemon.stub.add_process("node-a", 1, 4242, "someoneprivate")
+    daemon.infrastructure.publish("node-a", daemon.stub.sample("node-a"))
+    r = client.get("/api/metrics/prometheus")  # scrape target: no JWT
+    assert r.status_code == 200 and r.mimetype == "text/plain"
+    text = r.get_data(as_text=True)
+    assert 'tensorhive_gpu_metric{host="node-a",gpu="0"' in text
+    assert 'metric="power",unit="W"' in text
+    assert 'tensorhive_sample_age_seconds{host="node-a"}' in text
+    assert "someoneprivate" not in text and "4242" not in text
+    busy = [ln for ln in text.splitlines() if ln.startswith('tensorhive_gpu_processes{host="node-a",gpu="1"')]
+    assert busy and busy[0].endswith(" 1")
+    for ln in text.splitlines():  # every sample line is `name{labels} number`
+        if not ln.startswith("#"):
+            float(ln.rsplit(" ", 1)[1])

@@ -1,0 +1,68 @@
+"""AddressSanitizer + UndefinedBehaviorSanitizer runs of the native host tools (SURVEY §5 race /
+memory-error detection): the th-run supervisor's whole spawn / ls / status / wait / signal cycle,
+including its forked monitor process, and th-smi's start-up path, with every sanitizer report
+written to a file and asserted absent."""
+import os
+import shutil
+import subprocess
+import time
+
+import pytest
+
+from tensorhive_fixed_amd.native.build import _build_one, path_of, sanitizer_env
+
+pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++ with libasan")
+
+
+def _build(name):
+    _, err = _build_one(name, False)
+    if err and "libasan" in err:
+        pytest.skip("libasan not available")
+    assert err is None, err
+    return str(path_of(name))
+
+
+def _reports(d):
+    return {p: open(os.path.join(d, p)).read()[-2000:] for p in os.listdir(d)}
+
+
+def test_th_run_under_asan_ubsan(tmp_path):
+    th = _build("th-run-asan")
+    rep = tmp_path / "reports"
+    rep.mkdir()
+    env = {**os.environ, "TH_RUN_STATE_DIR": str(tmp_path / "state"), **sanitizer_env(str(rep))}
+
+    def run(*a, timeout=30):
+        return subprocess.run([th, *a], capture_output=True, text=True, env=env, timeout=timeout)
+
+    r = run("spawn", "--name", "tensorhive_task_a", "--log", str(tmp_path / "a.log"), "--env", "X=1", "--",
+            "bash", "-c", "echo $X; exit 3")
+    assert r.returncode == 0, r.stderr
+    assert run("wait", "--name", "tensorhive_task_a", "--timeout", "20").returncode == 3
+    r = run("spawn", "--name", "tensorhive_task_b", "--log", str(tmp_path / "b.log"), "--", "sleep", "60")
+    pid = int(r.stdout.strip())
+    ls = run("ls")
+    assert "tensorhive_task_b" in ls.stdout
+    assert '"running"' in run("status", "--name", "tensorhive_task_b").stdout.replace(" ", "")
+    assert run("terminate", "--name", "tensorhive_task_b").returncode == 0
+    assert run("wait", "--name", "tensorhive_task_b", "--timeout", "20").returncode != 0
+    assert run("kill", "--name", "tensorhive_task_nope").returncode != 0
+    assert run("bogus-subcommand").returncode != 0
+    # monitors write their reports when they exit
+    t0 = time.time()
+    while time.time() - t0 < 10 and os.path.exists(f"/proc/{pid}"):
+        time.sleep(0.1)
+    time.sleep(0.5)
+    assert (tmp_path / "a.log").read_text().strip() == "1"
+    assert _reports(rep) == {}
+
+
+def test_th_smi_startup_under_asan(tmp_path):
+    smi = _build("th-smi-asan")
+    rep = tmp_path / "reports"
+    rep.mkdir()
+    r = subprocess.run([smi], capture_output=True, text=True, timeout=60,
+                       env={**os.environ, **sanitizer_env(str(rep))})
+    # no GPU here: amdsmi init fails cleanly; on a GPU node it prints one JSON sample
+    assert r.returncode in (0, 1) and (r.returncode == 1 or r.stdout.startswith("{"))
+    assert _reports(rep) == {}
