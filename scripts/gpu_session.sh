@@ -23,6 +23,9 @@ for s in ${TH_STEPS:-tests bench}; do
     bench_small) step bench_small 600 python bench.py --model llama3-1b-shape --steps 3 --warmup 1 ;;
     bench) step bench 900 python bench.py --steps ${TH_BENCH_STEPS:-5} --warmup 2 ;;
     kbench) step kbench 600 python scripts/bench_kernels.py ;;
+    bench_plain) step bench_plain 900 env TH_DGRAD_NT=0 TH_WGRAD_NT=0 python bench.py --steps ${TH_BENCH_STEPS:-5} --warmup 2 ;;
+    transpose_bw) step transpose_bw 300 python scripts/transpose_bw.py ;;
+    layouts) step gemm_layouts 600 python scripts/gemm_layouts.py ;;
     flash) step flash_tests 600 python -m pytest tests/gpu/test_flash_attn_gpu.py -x -q ;;
     native) step native_tests 600 python -m pytest tests/gpu/test_native_gpu.py -x -q ;;
     doctor) step doctor 300 python -m tensorhive_fixed_amd doctor ;;

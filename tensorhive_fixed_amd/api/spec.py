@@ -196,6 +196,8 @@ EXTRA_OPERATIONS: list[Op] = [
     Op("GET", "/metrics/internal", "nodes.get_internal_metrics", "admin", tag="nodes"),            # new
     Op("GET", "/jobs/templates", "job.get_templates", "jwt", tag="jobs"),                         # new
     Op("GET", "/metrics/prometheus", "nodes.get_prometheus", None, tag="nodes"),                  # new
+    Op("PUT", "/jobs/{id}/reservation/{reservation_id}", "job.attach_to_reservation", "jwt",      # new
+       [P("id"), P("reservation_id"), Q("siblings", "boolean")], tag="jobs"),
 ]
 
 COMPAT_OPERATION_COUNT = 66

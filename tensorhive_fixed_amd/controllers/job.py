@@ -237,6 +237,63 @@ def business_stop(id: int, gracefully: bool | None = True):
     return {"msg": M("job.stop.success"), "job": job.as_dict()}, 200
 
 
+@guarded(not_found="job.not_found", forbidden="job.update.failure.forbidden",
+         assertion="job.update.failure.assertions")
+def attach_to_reservation(id: int, reservation_id: int, siblings: bool | None = True):
+    """Run a job inside a reservation (the reservation card's "attach jobs", reference
+    ``FullCalendarInfo.vue:510-548``), done server-side in one transaction: the job's window
+    becomes the reservation's, and every task moves to the reserved node with
+    ``HIP_VISIBLE_DEVICES`` set to the reserved GPUs' HIP indices in xGMI ring order
+    (``--nproc_per_node=`` follows).  ``siblings`` (default on) also takes the owner's other
+    reservations on the same node with the same window -- a multi-GPU reservation made in one
+    go -- so a torchrun task gets all of them.  The reference rewrote the first word of the
+    command to ``CUDA_VISIBLE_DEVICES=<one index>``, clobbering commands that had no prefix."""
+    from ..api.app import daemon
+    from ..core.launcher import devices_for_uuids, hip_visible_devices, order_for_rings
+    from ..models.orm import Reservation, Resource
+    from . import task as task_ctl
+
+    job = Job.get(id)
+    if not (is_admin() or job.user_id == me()):
+        raise ForbiddenException("not an owner")
+    assert job.status is not JobStatus.running, "must be stopped first"
+    res = Reservation.get(reservation_id)
+    assert res.user_id == job.user_id, "reservation belongs to another user"
+    assert not res.is_cancelled, "reservation is cancelled"
+    resource = Resource.get(res.resource_id)
+    chosen = [res]
+    if siblings is None or siblings:
+        for r in Reservation.query.filter(Reservation.user_id == res.user_id, Reservation.id != res.id).all():
+            if r.is_cancelled or r.start != res.start or r.end != res.end:
+                continue
+            other = Resource.query.filter(Resource.id == r.resource_id).first()
+            if other is not None and other.hostname == resource.hostname:
+                chosen.append(r)
+    d = daemon()
+    snap = d.infrastructure.snapshot().data if d is not None else {}
+    topo = d.topology().get(resource.hostname) if d is not None else None
+    try:
+        idx = devices_for_uuids(snap, resource.hostname, [r.resource_id for r in chosen])
+    except KeyError:
+        raise AssertionError("reserved GPUs are not visible on the node right now")
+    idx = order_for_rings(idx, topo)
+    job.start_at, job.stop_at = res.start, res.end
+    job.save()
+    for t in job.tasks:
+        assert t.status is not task_ctl.TaskStatus.running, "must be stopped first"
+        form = {"envs": [{"name": n, "value": v} for n, v in t.envs()
+                         if n not in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")],
+                "params": [{"name": n, "value": str(len(idx)) if n == "--nproc_per_node=" else v}
+                           for n, v in t.params()]}
+        form["envs"].insert(0, {"name": "HIP_VISIBLE_DEVICES", "value": hip_visible_devices(idx)})
+        words = t.command.split(" ")
+        command = " ".join(words[1:]) if words[0].startswith(("HIP_VISIBLE_DEVICES=", "CUDA_VISIBLE_DEVICES=",
+                                                               "ROCR_VISIBLE_DEVICES=")) else t.command
+        task_ctl.business_update(t.id, {"hostname": resource.hostname, "command": command, "cmdsegments": form})
+    _wake("job")
+    return {"msg": M("job.update.success"), "job": Job.get(id).as_dict()}, 200
+
+
 def get_templates():
     """Launch templates for the task creator (PyTorch-ROCm torchrun, TF_CONFIG, ClusterSpec)."""
     from ..core.launcher import TEMPLATES

@@ -96,7 +96,7 @@ class LlamaBlock(nn.Module):
         o = qkv_attention(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta)
         x = linear(o, self.wo, residual=x)
         h = rmsnorm(x, self.ffn_norm, c.norm_eps)
-        a = swiglu(linear(h, self.w13))
+        a = swiglu(linear(h, self.w13, wgrad_nt=True))
         return linear(a, self.w2, residual=x)
 
 

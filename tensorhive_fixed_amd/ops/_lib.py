@@ -42,6 +42,7 @@ _SIGS: dict[str, list] = {
     "th_flash_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, I, P],
     "th_embedding_bwd": [P, P, P, P, L, I, I, P],
     "th_probe_run": [P, I, I, I, P],
+    "th_transpose_bf16": [P, P, L, L, L, P],
 }
 
 

@@ -13,6 +13,8 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .linear import _DGRAD_NT
+from .transpose import transpose
 
 
 def ce_rows_(logits: torch.Tensor, target: torch.Tensor, grad_scale: float,
@@ -56,11 +58,13 @@ class _LinearCE(torch.autograd.Function):
         mg = getattr(w, "main_grad", None)
         acc = mg.view_as(w) if mg is not None else torch.zeros(w.shape, device=w.device, dtype=torch.float32)
         first_acc = mg is not None and not w.th_store.accumulating
+        # dh = dlogits @ W in the K-contiguous form (see ops/linear.py): one transpose of W per call
+        w_kn = transpose(w).t() if (h2.is_cuda and _DGRAD_NT) else w
         for i, s0 in enumerate(range(0, T, chunk)):
             hc = h2[s0: s0 + chunk]
             logits = torch.mm(hc, w.t())
             loss_sum += ce_rows_(logits, t[s0: s0 + chunk], scale, ignore_index).sum()
-            torch.mm(logits, w, out=dh[s0: s0 + chunk])
+            torch.mm(logits, w_kn, out=dh[s0: s0 + chunk])
             if mg is not None:
                 if i == 0 and first_acc:
                     torch.mm(logits.t(), hc, out=acc)
@@ -69,6 +73,7 @@ class _LinearCE(torch.autograd.Function):
             else:
                 acc.addmm_(logits.t().float(), hc.float())
             del logits
+        del w_kn
         if mg is not None:
             w.th_store.mark_ready(w)
             ctx.gw = None

@@ -4,17 +4,36 @@ GEMMs are plain library GEMMs (hipBLASLt through ``torch.mm``/``addmm``); what i
 data flow: the residual add of the attention-out and MLP-down projections is fused into the
 GEMM epilogue (``addmm`` with beta = 1), and ``dW = dYᵀ·X`` is written by the GEMM itself into
 ``weight.main_grad`` (see ``_grad.deliver``).
+
+Operand layouts (measured, ``scripts/gemm_layouts.py`` -> ``profiles/r01_gemm/``): hipBLASLt on
+gfx950 is fastest when both operands are contiguous along the reduction dim.  The forward
+``x @ Wᵀ`` already is; the input grad ``dY @ W`` is not, so W is transposed once per backward by
+a HIP kernel (``ops/transpose.py``, ~0.1 ms for the 235 MB gate|up weight) and the GEMM runs as
+``dY @ (Wᵀ)ᵀ`` -- 8-13 % faster.  For ``wgrad_nt`` layers (the gate|up projection, whose weight
+grad is the largest GEMM of the step) the weight grad runs as ``(dYᵀ) @ (Xᵀ)ᵀ`` on transposed
+copies of both operands: 6.29 -> 4.74 ms on the GEMM for ~0.9 ms of transposes.
+``TH_DGRAD_NT=0`` / ``TH_WGRAD_NT=0`` switch either back to the plain forms.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from ._grad import deliver, mm_into
+from .transpose import transpose
+
+_DGRAD_NT = os.environ.get("TH_DGRAD_NT", "1") == "1"
+_WGRAD_NT = os.environ.get("TH_WGRAD_NT", "1") == "1"
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous() else t.contiguous()
 
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None):
+    def forward(ctx, x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None, wgrad_nt: bool = False):
         x2 = x.reshape(-1, x.shape[-1])
         if residual is not None:
             y = torch.addmm(residual.reshape(-1, w.shape[0]), x2, w.t())
@@ -23,17 +42,27 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x2, w)
         ctx.has_res = residual is not None
         ctx.xshape = x.shape
+        ctx.wgrad_nt = wgrad_nt
         return y if x.dim() == 2 else y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy: torch.Tensor):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
-        dx = torch.mm(dy2, w).view(ctx.xshape)
-        gw = deliver(w, mm_into(dy2.t(), x2), lambda: torch.mm(dy2.t(), x2))
-        return dx, gw, (dy if ctx.has_res else None)
+        if dy2.is_cuda and _DGRAD_NT:
+            dx = torch.mm(dy2, transpose(w).t())
+        else:
+            dx = torch.mm(dy2, w)
+        dx = dx.view(ctx.xshape)
+        if ctx.wgrad_nt and dy2.is_cuda and _WGRAD_NT:
+            dyT, xT = transpose(_c(dy2)), transpose(_c(x2))
+            gw = deliver(w, mm_into(dyT, xT.t()), lambda: torch.mm(dyT, xT.t()))
+        else:
+            gw = deliver(w, mm_into(dy2.t(), x2), lambda: torch.mm(dy2.t(), x2))
+        return dx, gw, (dy if ctx.has_res else None), None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None,
+           wgrad_nt: bool = False) -> torch.Tensor:
     """``y = x @ w.T (+ residual)`` with weight-grad delivery into the flat buffer."""
-    return _Linear.apply(x, w, residual)
+    return _Linear.apply(x, w, residual, wgrad_nt)

@@ -60,3 +60,58 @@ def test_prometheus_exposition(client, daemon):
     for ln in text.splitlines():  # every sample line is `name{labels} number`
         if not ln.startswith("#"):
             float(ln.rsplit(" ", 1)[1])
+
+
+def test_attach_job_to_multi_gpu_reservation(client, daemon, new_user, new_user_2, auth_headers):
+    """Reservation card 'attach jobs' (FullCalendarInfo.vue:510-548), server side: job window :=
+    reservation window; tasks move to the node with HIP_VISIBLE_DEVICES = all reserved GPUs."""
+    from tensorhive_fixed_amd.core.launcher import torchrun_task
+    from tensorhive_fixed_amd.models.orm import Job, Reservation, Resource, Task
+
+    stub = daemon.stub
+    daemon.infrastructure.publish("node-b", stub.sample("node-b"))
+    start = datetime.datetime.utcnow() + datetime.timedelta(hours=1)
+    end = start + datetime.timedelta(hours=3)
+    res = []
+    for i in (5, 2):
+        u = stub.gpu_uuid("node-b", i)
+        Resource(id=u, name="MI355X", hostname="node-b").save()
+        r = Reservation(user_id=new_user.id, title="gang", description="", resource_id=u, start=start, end=end)
+        r.save()
+        res.append(r)
+    other = stub.gpu_uuid("node-b", 7)
+    Resource(id=other, name="MI355X", hostname="node-b").save()
+    Reservation(user_id=new_user.id, title="later", description="", resource_id=other,
+                start=end, end=end + datetime.timedelta(hours=1)).save()  # different window: not a sibling
+
+    job = Job(name="train", description="", user_id=new_user.id)
+    job.save()
+    form = torchrun_task("node-a", [0], "node-a")
+    st, data = api(client, "post", f"/jobs/{job.id}/tasks", auth_headers(new_user),
+                   {"hostname": "node-a", "command": "CUDA_VISIBLE_DEVICES=0 " + form["command"],
+                    "cmdsegments": form["cmdsegments"]})
+    assert st == 201, data
+    st, data = api(client, "post", f"/jobs/{job.id}/tasks", auth_headers(new_user),
+                   {"hostname": "node-a", "command": "python eval.py", "cmdsegments": {"envs": [], "params": []}})
+    assert st == 201, data
+
+    st, data = api(client, "put", f"/jobs/{job.id}/reservation/{res[0].id}", auth_headers(new_user_2))
+    assert st == 403
+    st, data = api(client, "put", f"/jobs/{job.id}/reservation/{res[0].id}", auth_headers(new_user))
+    assert st == 200, data
+    j = Job.get(job.id)
+    assert j.start_at == start.replace(microsecond=0) or abs((j.start_at - start).total_seconds()) < 1
+    for t in j.tasks:
+        t = Task.get(t.id)
+        assert t.hostname == "node-b"
+        assert t.full_command.startswith("HIP_VISIBLE_DEVICES=2,5 ")
+        assert "CUDA_VISIBLE_DEVICES" not in t.full_command
+        assert t.gpu_id == 2
+    torchrun = next(Task.get(t.id) for t in j.tasks if "torchrun" in Task.get(t.id).full_command)
+    assert "--nproc_per_node=2" in torchrun.full_command
+    assert "python eval.py" in next(Task.get(t.id).full_command for t in j.tasks if t.id != torchrun.id)
+
+    # only its own reservation; a single-GPU attach without siblings
+    st, _ = api(client, "put", f"/jobs/{job.id}/reservation/{res[1].id}", auth_headers(new_user), siblings="false")
+    assert st == 200
+    assert all(Task.get(t.id).full_command.startswith("HIP_VISIBLE_DEVICES=2 ") for t in Job.get(job.id).tasks)
