@@ -72,7 +72,11 @@ def _with_age(content, status=200):
     snap = _snapshot()
     resp = Response(json.dumps(content, default=str), status=status, mimetype="application/json")
     if snap is not None and snap.sampled_at:
-        resp.headers["X-Sample-Age-Ms"] = str(int(1000 * (time.time() - min(snap.sampled_at.values()))))
+        now = time.time()
+        resp.headers["X-Sample-Age-Ms"] = str(int(1000 * (now - min(snap.sampled_at.values()))))
+        # per host, so the dashboard can flag one stale node (heartbeat freshness)
+        resp.headers["X-Host-Sample-Age-Ms"] = ",".join(f"{h}={int(1000 * (now - t))}"
+                                                        for h, t in sorted(snap.sampled_at.items()))
     return resp
 
 

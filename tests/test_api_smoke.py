@@ -115,3 +115,15 @@ def test_attach_job_to_multi_gpu_reservation(client, daemon, new_user, new_user_
     st, _ = api(client, "put", f"/jobs/{job.id}/reservation/{res[1].id}", auth_headers(new_user), siblings="false")
     assert st == 200
     assert all(Task.get(t.id).full_command.startswith("HIP_VISIBLE_DEVICES=2 ") for t in Job.get(job.id).tasks)
+
+
+def test_per_host_sample_age_header(client, daemon, new_admin, auth_headers):
+    import time
+
+    daemon.infrastructure.publish("node-a", daemon.stub.sample("node-a"))
+    daemon.infrastructure.publish("node-b", daemon.stub.sample("node-b"), sampled_at=time.time() - 60)
+    r = client.get("/api/nodes/metrics", headers=auth_headers(new_admin))
+    assert r.status_code == 200
+    ages = dict(kv.rsplit("=", 1) for kv in r.headers["X-Host-Sample-Age-Ms"].split(","))
+    assert int(ages["node-a"]) < 5000 and 59000 <= int(ages["node-b"]) < 70000
+    assert int(r.headers["X-Sample-Age-Ms"]) >= 59000  # the oldest host
