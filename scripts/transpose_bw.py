@@ -1,8 +1,12 @@
 """Achieved HBM bandwidth of the HIP bf16 transpose vs torch's ``.t().contiguous()`` on the
 training-step shapes (read + write bytes / time)."""
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from tensorhive_fixed_amd.ops import _lib
 from tensorhive_fixed_amd.ops.transpose import transpose

@@ -16,6 +16,7 @@ Every weight gradient is written by its producing GEMM/kernel into the flat DDP 
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -76,6 +77,11 @@ class LlamaConfig:
         return 6 * n_mat + 3 * attn
 
 
+# projections whose weight grad runs on transposed operand copies (ops/linear.py): where the GEMM
+# speed-up outweighs the transposes (measured: profiles/r01_gemm/)
+WGRAD_NT = set(filter(None, os.environ.get("TH_WGRAD_NT_LAYERS", "w13").split(",")))
+
+
 class LlamaBlock(nn.Module):
     def __init__(self, cfg: LlamaConfig, device, dtype):
         super().__init__()
@@ -92,12 +98,12 @@ class LlamaBlock(nn.Module):
     def forward(self, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
         c = self.cfg
         h = rmsnorm(x, self.attn_norm, c.norm_eps)
-        qkv = linear(h, self.wqkv)
+        qkv = linear(h, self.wqkv, wgrad_nt="wqkv" in WGRAD_NT)
         o = qkv_attention(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta)
-        x = linear(o, self.wo, residual=x)
+        x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT)
         h = rmsnorm(x, self.ffn_norm, c.norm_eps)
-        a = swiglu(linear(h, self.w13, wgrad_nt=True))
-        return linear(a, self.w2, residual=x)
+        a = swiglu(linear(h, self.w13, wgrad_nt="w13" in WGRAD_NT))
+        return linear(a, self.w2, residual=x, wgrad_nt="w2" in WGRAD_NT)
 
 
 class Llama(nn.Module):

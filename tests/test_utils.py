@@ -248,3 +248,41 @@ def test_verifier_schedule_clamped_to_restriction_end():
     r = _R(D0, D0 + timedelta(hours=12), schedules=[always], resources=["R"])
     assert _allowed([r], D0 + timedelta(hours=1), D0 + timedelta(hours=11))
     assert not _allowed([r], D0 + timedelta(hours=1), D0 + timedelta(hours=13))
+
+
+def test_config_accepts_both_secret_key_spellings(tmp_path):
+    """the reference reads ``[auth] secrect_key`` (typo, config.py:289); both spellings work."""
+    from tensorhive_fixed_amd import config as C
+
+    C.init_config_files(tmp_path)
+    main = (tmp_path / "main_config.ini").read_text()
+    import re
+
+    main = re.sub(r"(?m)^secre[c]?t_key\s*=.*$", "", main)
+    (tmp_path / "main_config.ini").write_text(main + "\n[auth]\nsecrect_key = typo-spelling\n"
+                                              if "[auth]" not in main else
+                                              main.replace("[auth]", "[auth]\nsecrect_key = typo-spelling"))
+    assert C.load_config(tmp_path).auth.secret_key == "typo-spelling"
+    main2 = (tmp_path / "main_config.ini").read_text().replace("secrect_key", "secret_key")
+    (tmp_path / "main_config.ini").write_text(main2)
+    assert C.load_config(tmp_path).auth.secret_key == "typo-spelling"
+
+
+def test_global_restrictions_exclude_expired(tables):
+    """the reference discards its ``include_expired`` filter (Restriction.py:190-193)."""
+    import datetime
+
+    from tensorhive_fixed_amd.models.orm import Restriction
+
+    now = datetime.datetime.utcnow()
+    live = Restriction(name="live", starts_at=now - datetime.timedelta(days=2), is_global=True)
+    live.save()
+    old = Restriction(name="old", starts_at=now - datetime.timedelta(days=9), ends_at=now + datetime.timedelta(days=1),
+                      is_global=True)
+    old.save()
+    from tensorhive_fixed_amd.database import db_session
+
+    old._ends_at = now - datetime.timedelta(days=1)  # expire it behind the model's edit guard
+    db_session.commit()
+    assert [r.name for r in Restriction.get_global_restrictions()] == ["live"]
+    assert sorted(r.name for r in Restriction.get_global_restrictions(include_expired=True)) == ["live", "old"]
