@@ -30,10 +30,14 @@ def t(fn, it=20):
 for R, C in ((32768, 28672), (32768, 4096), (28672, 4096), (4096, 14336), (4096, 6144), (128256, 4096)):
     x = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
     out = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
-    ms_k = t(lambda: transpose(x, out))
-    ms_t = t(lambda: out.copy_(x.t()))
     gb = 2 * x.numel() * 2 / 1e9
-    print(json.dumps({"R": R, "C": C, "hip_ms": round(ms_k, 4), "hip_TBps": round(gb / ms_k, 2),
-                      "torch_ms": round(ms_t, 4), "torch_TBps": round(gb / ms_t, 2)}), flush=True)
+    res = {"R": R, "C": C}
+    for tile in (0, 2, 3):
+        ms_k = t(lambda: transpose(x, out, tile=tile))
+        assert torch.equal(out, x.t())
+        res[f"tile{tile}_TBps"] = round(gb / ms_k, 2)
+    ms_t = t(lambda: out.copy_(x.t()))
+    res["torch_TBps"] = round(gb / ms_t, 2)
+    print(json.dumps(res), flush=True)
     del x, out
     torch.cuda.empty_cache()

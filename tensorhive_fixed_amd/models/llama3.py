@@ -26,7 +26,8 @@ from ..ops.attention import qkv_attention
 from ..ops.cross_entropy import linear_cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import linear
-from ..ops.rmsnorm import rmsnorm
+from ..ops.mlp import gate_up_swiglu
+from ..ops.rmsnorm import rmsnorm, rmsnorm_fork
 from ..ops.swiglu import swiglu
 
 
@@ -97,12 +98,16 @@ class LlamaBlock(nn.Module):
 
     def forward(self, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
         c = self.cfg
-        h = rmsnorm(x, self.attn_norm, c.norm_eps)
+        # rmsnorm_fork: the residual gradient is added inside the RMSNorm backward kernel
+        h, x = rmsnorm_fork(x, self.attn_norm, c.norm_eps)
         qkv = linear(h, self.wqkv, wgrad_nt="wqkv" in WGRAD_NT)
         o = qkv_attention(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta)
         x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT)
-        h = rmsnorm(x, self.ffn_norm, c.norm_eps)
-        a = swiglu(linear(h, self.w13, wgrad_nt="w13" in WGRAD_NT))
+        h, x = rmsnorm_fork(x, self.ffn_norm, c.norm_eps)
+        if "w13" in WGRAD_NT:  # fused gate|up + SwiGLU node: transposed dGU from the SwiGLU kernel
+            a = gate_up_swiglu(h, self.w13)
+        else:
+            a = swiglu(linear(h, self.w13))
         return linear(a, self.w2, residual=x, wgrad_nt="w2" in WGRAD_NT)
 
 

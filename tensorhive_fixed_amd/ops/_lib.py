@@ -31,9 +31,10 @@ F = C.c_float
 # name -> argtypes (every function returns int: 0 = ok, <0 = rejected shape, >0 = hipError)
 _SIGS: dict[str, list] = {
     "th_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
-    "th_rmsnorm_bwd": [P, P, P, P, P, P, P, I, I, I, I, P],
+    "th_rmsnorm_bwd": [P, P, P, P, P, P, P, I, I, I, I, P, P],
     "th_swiglu_fwd": [P, P, L, I, P],
     "th_swiglu_bwd": [P, P, P, L, I, P],
+    "th_swiglu_bwd_t": [P, P, P, P, L, I, P],
     "th_rope_inplace": [P, P, P, L, I, I, I, I, F, P],
     "th_sumsq_bf16": [P, L, P, P, I, P],
     "th_adamw_step": [P, P, P, P, P, L, F, F, F, F, F, I, F, P, F, P],
@@ -42,7 +43,7 @@ _SIGS: dict[str, list] = {
     "th_flash_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, I, P],
     "th_embedding_bwd": [P, P, P, P, L, I, I, P],
     "th_probe_run": [P, I, I, I, P],
-    "th_transpose_bf16": [P, P, L, L, L, P],
+    "th_transpose_bf16": [P, P, L, L, L, I, P],
 }
 
 

@@ -57,7 +57,10 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const ushort* __restri
                                                           const ushort* __restrict__ w,
                                                           const float* __restrict__ rstd,
                                                           ushort* __restrict__ dx,
-                                                          float* __restrict__ ws, int T, int D) {
+                                                          float* __restrict__ ws, int T, int D,
+                                                          const ushort* __restrict__ dres) {
+  // dres (optional): gradient arriving through the residual branch of the same x, added into dx
+  // here instead of by a separate elementwise pass (ops/rmsnorm.py: rmsnorm_fork)
   __shared__ float red[16];
   const int nvec = D >> 3;
   float dwacc[MAXV][8];
@@ -76,7 +79,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const ushort* __restri
   for (int row = blockIdx.x; row < T; row += gridDim.x) {
     const ushort8* xr = reinterpret_cast<const ushort8*>(x + (size_t)row * D);
     const ushort8* gr = reinterpret_cast<const ushort8*>(dy + (size_t)row * D);
-    ushort8 xc[MAXV], gc[MAXV];
+    ushort8 xc[MAXV], gc[MAXV], rc[MAXV];
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
@@ -84,6 +87,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const ushort* __restri
       if (v < nvec) {
         xc[i] = xr[v];
         gc[i] = gr[v];
+        rc[i] = dres ? reinterpret_cast<const ushort8*>(dres + (size_t)row * D)[v] : ushort8(0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) dot += bf2f(gc[i][j]) * wreg[i][j] * bf2f(xc[i][j]);
       }
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const ushort* __restri
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xf = bf2f(xc[i][j]), gf = bf2f(gc[i][j]);
-          o[j] = f2bf(r * gf * wreg[i][j] - xf * c);
+          o[j] = f2bf(r * gf * wreg[i][j] - xf * c + bf2f(rc[i][j]));
           dwacc[i][j] += gf * xf * r;
         }
         dxr[v] = o;
@@ -151,16 +155,16 @@ extern "C" int th_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd
 // Workspace: nblk * D floats; nblk chosen by the caller (<= T), typically 2 * 256 CUs.
 extern "C" int th_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
                               void* dx, void* dw, float* ws, int nblk, int T, int D,
-                              int accumulate, hipStream_t s) {
+                              int accumulate, const void* dres, hipStream_t s) {
   if (D % 8 != 0 || T <= 0 || nblk <= 0) return -1;
   const int mv = pick_maxv(D, 256);
   dim3 g(nblk), b(256);
   if (mv <= 2)
-    rmsnorm_bwd_kernel<2><<<g, b, 0, s>>>((const ushort*)dy, (const ushort*)x, (const ushort*)w, rstd, (ushort*)dx, ws, T, D);
+    rmsnorm_bwd_kernel<2><<<g, b, 0, s>>>((const ushort*)dy, (const ushort*)x, (const ushort*)w, rstd, (ushort*)dx, ws, T, D, (const ushort*)dres);
   else if (mv <= 4)
-    rmsnorm_bwd_kernel<4><<<g, b, 0, s>>>((const ushort*)dy, (const ushort*)x, (const ushort*)w, rstd, (ushort*)dx, ws, T, D);
+    rmsnorm_bwd_kernel<4><<<g, b, 0, s>>>((const ushort*)dy, (const ushort*)x, (const ushort*)w, rstd, (ushort*)dx, ws, T, D, (const ushort*)dres);
   else if (mv <= 8)
-    rmsnorm_bwd_kernel<8><<<g, b, 0, s>>>((const ushort*)dy, (const ushort*)x, (const ushort*)w, rstd, (ushort*)dx, ws, T, D);
+    rmsnorm_bwd_kernel<8><<<g, b, 0, s>>>((const ushort*)dy, (const ushort*)x, (const ushort*)w, rstd, (ushort*)dx, ws, T, D, (const ushort*)dres);
   else
     return -2;
   slab_reduce_bf16_kernel<<<dim3((D + 255) / 256), dim3(256), 0, s>>>(ws, (ushort*)dw, nblk, D, accumulate);

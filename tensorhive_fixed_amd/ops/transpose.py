@@ -4,10 +4,14 @@ from __future__ import annotations
 
 import torch
 
+import os
+
 from . import _lib
 
+_TILE = int(os.environ.get("TH_TRANSPOSE_TILE", "0"))
 
-def transpose(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+
+def transpose(x: torch.Tensor, out: torch.Tensor | None = None, tile: int | None = None) -> torch.Tensor:
     if x.dim() != 2:
         raise ValueError("transpose expects a 2-D tensor")
     R, C = x.shape
@@ -21,5 +25,6 @@ def transpose(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
                          f"{tuple(x.shape)} {x.dtype} strides {x.stride()}")
     if not out.is_contiguous() or tuple(out.shape) != (C, R):
         raise ValueError("out must be a contiguous [C, R] tensor")
-    _lib.call("th_transpose_bf16", x.data_ptr(), out.data_ptr(), R, C, x.stride(0), _lib.stream_ptr(x.device))
+    _lib.call("th_transpose_bf16", x.data_ptr(), out.data_ptr(), R, C, x.stride(0), _TILE if tile is None else tile,
+              _lib.stream_ptr(x.device))
     return out

@@ -185,3 +185,58 @@ def test_linear_nt_backward_matches_plain_forms():
     ref_dw = g.float().t() @ x.float()
     _close(x.grad, ref_dx, 0.5, 1e-2)
     _close(w.grad, ref_dw, 0.5, 1e-2)
+
+
+@pytest.mark.parametrize("T,F", [(256, 64), (4096, 1024), (200, 128)])
+def test_swiglu_bwd_transposed_output(T, F):
+    from tensorhive_fixed_amd.ops import _lib
+    torch.manual_seed(9)
+    gu = torch.randn(T, 2 * F, device=DEV, dtype=torch.bfloat16)
+    d = torch.randn(T, F, device=DEV, dtype=torch.bfloat16)
+    dgu = torch.empty_like(gu)
+    dguT = torch.empty(2 * F, T, device=DEV, dtype=torch.bfloat16)
+    _lib.call("th_swiglu_bwd_t", d.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, F,
+              _lib.stream_ptr(gu.device))
+    g, u = gu.float().chunk(2, -1)
+    s = torch.sigmoid(g)
+    ref = torch.cat([d.float() * u * s * (1 + g * (1 - s)), d.float() * g * s], -1)
+    _close(dgu, ref, 2e-2, 1e-2)
+    assert torch.equal(dguT, dgu.t())
+
+
+def test_gate_up_swiglu_matches_unfused():
+    from tensorhive_fixed_amd.ops.linear import linear
+    from tensorhive_fixed_amd.ops.mlp import gate_up_swiglu
+    from tensorhive_fixed_amd.ops.swiglu import swiglu
+    torch.manual_seed(10)
+    T, D, F = 512, 256, 512
+    h = torch.randn(T, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(2 * F, D, device=DEV, dtype=torch.bfloat16) * 0.05).requires_grad_(True)
+    g = torch.randn(T, F, device=DEV, dtype=torch.bfloat16)
+    a = gate_up_swiglu(h, w)
+    a.backward(g)
+    h2, w2 = h.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
+    swiglu(linear(h2, w2)).backward(g)
+    _close(a, swiglu(linear(h2.detach(), w2.detach())), 1e-2, 1e-2)
+    _close(h.grad, h2.grad, 5e-2, 2e-2)
+    _close(w.grad, w2.grad, 5e-2, 2e-2)
+
+
+def test_rmsnorm_fork_fuses_residual_gradient():
+    from tensorhive_fixed_amd.ops.rmsnorm import rmsnorm, rmsnorm_fork
+    torch.manual_seed(11)
+    T, D = 300, 4096
+    x = torch.randn(T, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(D, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    gh, gr = torch.randn(T, D, device=DEV, dtype=torch.bfloat16), torch.randn(T, D, device=DEV, dtype=torch.bfloat16)
+    h, xr = rmsnorm_fork(x, w)
+    assert xr.data_ptr() == x.data_ptr()
+    torch.autograd.backward([h, xr], [gh, gr])
+    xf = x.detach().float().requires_grad_(True)
+    wf = w.detach().float().requires_grad_(True)
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    torch.autograd.backward([ref, xf], [gh.float(), gr.float()])
+    _close(h, ref, 3e-2, 1e-2)
+    _close(x.grad, xf.grad, 5e-2, 1e-2)
+    _close(w.grad, wf.grad, 0.5, 1e-2)
+    assert rmsnorm is not None

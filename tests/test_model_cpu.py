@@ -69,3 +69,21 @@ def test_custom_op_model_matches_reference_cpu():
 
 def test_param_count_llama3_8b():
     assert LlamaConfig.llama3_8b().num_params() == 8_030_261_248
+
+
+def test_gate_up_swiglu_cpu_matches_unfused():
+    import torch
+
+    from tensorhive_fixed_amd.ops.linear import linear
+    from tensorhive_fixed_amd.ops.mlp import gate_up_swiglu
+    from tensorhive_fixed_amd.ops.swiglu import swiglu
+
+    torch.manual_seed(0)
+    h = torch.randn(64, 32, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(128, 32, dtype=torch.bfloat16) * 0.1).requires_grad_(True)
+    g = torch.randn(64, 64, dtype=torch.bfloat16)
+    gate_up_swiglu(h, w).backward(g)
+    h2, w2 = h.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
+    swiglu(linear(h2, w2)).backward(g)
+    assert torch.allclose(h.grad.float(), h2.grad.float(), atol=3e-2, rtol=2e-2)
+    assert torch.allclose(w.grad.float(), w2.grad.float(), atol=3e-2, rtol=2e-2)
