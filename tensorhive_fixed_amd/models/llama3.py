@@ -81,6 +81,13 @@ class LlamaConfig:
 # projections whose weight grad runs on transposed operand copies (ops/linear.py): where the GEMM
 # speed-up outweighs the transposes (measured: profiles/r01_gemm/)
 WGRAD_NT = set(filter(None, os.environ.get("TH_WGRAD_NT_LAYERS", "w13").split(",")))
+_FORK = os.environ.get("TH_RMSNORM_FORK", "1") == "1"
+
+
+def _norm(x, w, eps):
+    if _FORK:
+        return rmsnorm_fork(x, w, eps)
+    return rmsnorm(x, w, eps), x
 
 
 class LlamaBlock(nn.Module):
@@ -99,11 +106,11 @@ class LlamaBlock(nn.Module):
     def forward(self, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
         c = self.cfg
         # rmsnorm_fork: the residual gradient is added inside the RMSNorm backward kernel
-        h, x = rmsnorm_fork(x, self.attn_norm, c.norm_eps)
+        h, x = _norm(x, self.attn_norm, c.norm_eps)
         qkv = linear(h, self.wqkv, wgrad_nt="wqkv" in WGRAD_NT)
         o = qkv_attention(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta)
         x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT)
-        h, x = rmsnorm_fork(x, self.ffn_norm, c.norm_eps)
+        h, x = _norm(x, self.ffn_norm, c.norm_eps)
         if "w13" in WGRAD_NT:  # fused gate|up + SwiGLU node: transposed dGU from the SwiGLU kernel
             a = gate_up_swiglu(h, self.w13)
         else:
