@@ -53,7 +53,7 @@ def bwd_time(qkv, B, S, Hq, Hkv, D, flops):
     o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
     do = torch.randn_like(o)
     ref = None
-    for flags in (4, 0, 4, 0, 4, 0):
+    for flags in [int(f) for f in os.environ.get("BWD_FLAGS", "0,8,0,8").split(",")]:
         ts = []
         for _ in range(5):
             s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
