@@ -1,0 +1,35 @@
+"""bench.py contract (driver): ``torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W``
+prints ONE JSON line from rank 0 with the whole-job value.  Rehearsed here with 2 gloo ranks on the
+CPU and the tiny model (the 8-GPU RCCL run is the driver's)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_bench_prints_one_json_line(tmp_path):
+    env = {**os.environ, "TH_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "2"}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "tiny", "--seq-len", "64",
+                        "--micro-batch", "2"], capture_output=True, text=True, env=env, timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    # whole-job aggregate: tokens of both ranks over the (max-over-ranks) step time
+    assert abs(d["value"] - 2 * 2 * 64 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
