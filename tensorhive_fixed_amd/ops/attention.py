@@ -95,8 +95,8 @@ def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.T
     if not do.is_contiguous():
         do = do.contiguous()
     dqkv = torch.empty_like(qkv)
-    # f32 dQ accumulator (atomics across key blocks) + delta = rowsum(dO * O) scratch
-    dq_acc = torch.zeros((B * S, Hq * Dh), device=qkv.device, dtype=torch.float32)
+    # delta = rowsum(dO * O) scratch (dQ is computed by its own query-centric kernel: no f32
+    # accumulator, no atomics)
     delta = torch.empty((B, Hq, S), device=qkv.device, dtype=torch.float32)
     q = qkv.data_ptr()
     k = q + Hq * Dh * 2
@@ -105,7 +105,7 @@ def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.T
     dk = dq + Hq * Dh * 2
     dv = dk + Hkv * Dh * 2
     _lib.call("th_flash_attn_bwd", q, k, v, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
-              delta.data_ptr(), dq_acc.data_ptr(), dq, dk, dv, B, S, Hq, Hkv, Dh, int(causal), row,
+              delta.data_ptr(), None, dq, dk, dv, B, S, Hq, Hkv, Dh, int(causal), row,
               S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), int(flags), _lib.stream_ptr(qkv.device))
     return dqkv
 
