@@ -231,20 +231,45 @@ def bench(what, requests, gpus):
         click.echo(json.dumps(benchmarks.train_throughput(gpus)))
 
 
+def rocprof_prefix(task_id: int, pmc: str = "") -> str:
+    """rocprofv3 in front of a task's program.  Counters (``--pmc``) get their own run without
+    tracing; the output lands next to the task logs."""
+    if pmc:
+        return ("rocprofv3 --pmc %s --output-format csv -d ~/TensorHiveLogs/pmc_task_%d"
+                % (pmc.replace(",", " "), task_id))
+    return "rocprofv3 --kernel-trace --stats --output-format csv -d ~/TensorHiveLogs/prof_task_%d" % task_id
+
+
 @main.command()
 @click.option("--task", "task_id", required=True, type=int)
 @click.option("--pmc", default="", help="comma separated counters (separate run, never with tracing)")
-def profile(task_id, pmc):
-    """Print the rocprofv3 command that profiles a task's command (kernel trace + stats)."""
+@click.option("--create", is_flag=True, help="add the profiled copy as a new task of the same job")
+def profile(task_id, pmc, create):
+    """Profile a task under rocprofv3 (kernel trace + stats, or --pmc counters).
+
+    Prints the profiled command line.  The task's environment segments stay in front of
+    rocprofv3 and the program itself follows ``--``, because rocprofv3 must start the program
+    directly.  ``--create`` stores it as a new task of the same job, ready to run or enqueue."""
     from .database import configure
     from .models.orm import Task
 
     configure()
     t = Task.get(task_id)
-    pre = "rocprofv3 --kernel-trace --stats --output-format csv -d ~/TensorHiveLogs/prof_task_%d" % task_id
-    if pmc:
-        pre = "rocprofv3 --pmc %s --output-format csv -d ~/TensorHiveLogs/pmc_task_%d" % (pmc.replace(",", " "), task_id)
-    click.echo(f"{pre} -- {t.full_command}")
+    prof = rocprof_prefix(task_id, pmc)
+    envs = " ".join(f"{n}={v}" for n, v in t.envs())
+    body = t.full_command[len(envs):].strip() if envs and t.full_command.startswith(envs) else t.full_command
+    click.echo(f"{envs} {prof} -- {body}".strip())
+    if create:
+        from .controllers.task import _apply_segments
+
+        nt = Task(command=f"{prof} -- {t.command}", hostname=t.hostname)
+        nt.save()
+        _apply_segments(nt, {"envs": [{"name": n, "value": v} for n, v in t.envs()],
+                             "params": [{"name": n, "value": v} for n, v in t.params()]})
+        nt.save()
+        if t.job is not None:
+            t.job.add_task(nt)
+        click.echo(f"created task {nt.id}")
 
 
 if __name__ == "__main__":

@@ -84,6 +84,24 @@ def test_cli_profile_prints_rocprof_line(cfg, tables, monkeypatch, new_job_with_
     assert "--pmc SQ_WAVES GRBM_COUNT" in r.output and "--kernel-trace" not in r.output
 
 
+def test_cli_profile_keeps_env_in_front_and_creates_task(cfg, tables, monkeypatch, new_job_with_task, new_task_2):
+    """rocprofv3 must start the program itself: env assignments go before it, never after `--`."""
+    from tensorhive_fixed_amd.cli import main
+    from tensorhive_fixed_amd.models.orm import Job, Task
+
+    monkeypatch.setattr("tensorhive_fixed_amd.database.configure", lambda *a, **k: None)
+    job = new_job_with_task
+    job.add_task(new_task_2)
+    r = CliRunner().invoke(main, ["-c", str(cfg.directory), "profile", "--task", str(new_task_2.id), "--create"])
+    assert r.exit_code == 0, r.output
+    line = r.output.splitlines()[0]
+    assert line.startswith("HIP_VISIBLE_DEVICES=0 rocprofv3 --kernel-trace") and line.endswith("-- python eval.py")
+    new_id = int(r.output.splitlines()[1].split()[-1])
+    t = Task.get(new_id)
+    assert t.full_command == line and t.hostname == "node-b" and t.gpu_id == 0
+    assert new_id in [x.id for x in Job.get(job.id).tasks]
+
+
 def test_cli_test_command_with_simulated_nodes(cfg):
     from tensorhive_fixed_amd.cli import main
 
