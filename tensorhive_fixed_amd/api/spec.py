@@ -62,6 +62,10 @@ SCHEMAS: dict[str, dict] = {
     "TaskForm": {"required": ["command", "hostname"],
                  "properties": {"jobId": "integer", "command": "string", "hostname": "string", "cmdsegments": "object"}},
     "TaskUpdateForm": {"required": [], "properties": {"command": "string", "hostname": "string", "cmdsegments": "object"}},
+    # new: multi-task launch generator (torchrun / torch TCP ranks / TF2 TF_CONFIG / TF1 ClusterSpec)
+    "TaskGenerateForm": {"required": ["template", "placements"],
+                         "properties": {"template": "string", "command": "string", "module": "string",
+                                        "placements": "array", "masterPort": "integer"}},
     "JobForm": {"required": ["name", "userId"],
                 "properties": {"name": "string", "description": "string", "userId": "integer", "startAt": "string?",
                                "stopAt": "string?"}},
@@ -196,6 +200,8 @@ EXTRA_OPERATIONS: list[Op] = [
     Op("GET", "/metrics/internal", "nodes.get_internal_metrics", "admin", tag="nodes"),            # new
     Op("GET", "/jobs/templates", "job.get_templates", "jwt", tag="jobs"),                         # new
     Op("GET", "/metrics/prometheus", "nodes.get_prometheus", None, tag="nodes"),                  # new
+    Op("POST", "/jobs/{id}/tasks/generate", "job.generate_tasks", "jwt", [P("id")],              # new
+       body="TaskGenerateForm", body_name="form", tag="jobs"),
     Op("PUT", "/jobs/{id}/reservation/{reservation_id}", "job.attach_to_reservation", "jwt",      # new
        [P("id"), P("reservation_id"), Q("siblings", "boolean")], tag="jobs"),
 ]

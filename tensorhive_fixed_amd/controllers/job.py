@@ -294,6 +294,65 @@ def attach_to_reservation(id: int, reservation_id: int, siblings: bool | None = 
     return {"msg": M("job.update.success"), "job": Job.get(id).as_dict()}, 200
 
 
+def _placements(form: dict) -> list[dict]:
+    out = []
+    for p in form["placements"]:
+        assert isinstance(p, dict) and isinstance(p.get("hostname"), str), "placement needs a hostname"
+        gpus = p.get("gpus", [p["gpu"]] if "gpu" in p else [])
+        assert all(isinstance(g, int) and g >= 0 for g in gpus), "gpus must be device indices"
+        out.append({"hostname": p["hostname"], "gpus": gpus, "role": p.get("role", "worker")})
+    assert out, "no placements"
+    return out
+
+
+@guarded(not_found="job.not_found", forbidden="job.update.failure.forbidden",
+         assertion="task.create.failure.invalid")
+def generate_tasks(id: int, form: dict):
+    """Create every task of a distributed launch in one call (the reference's task creator did
+    this in the browser, ``TaskCreate.vue:201-215,617-670``, and never persisted TF_CONFIG).
+
+    ``template``: ``torchrun`` (one task per host, all its GPUs, c10d rendezvous on the first
+    host), ``torch`` (one task per GPU with explicit ``--rank``/``--world-size``), ``tf2``
+    (TF_CONFIG per task, ports auto-increment per host from 2222; ``role`` chief/worker/ps/
+    evaluator), ``tf1`` (ClusterSpec ``--ps_hosts/--worker_hosts``; ``role`` ps/worker).
+    ``placements``: ``[{"hostname": h, "gpus": [i, ...] | "gpu": i, "role": r}]``."""
+    from ..core import launcher
+    from . import task as task_ctl
+
+    job = Job.get(id)
+    if not (is_admin() or job.user_id == me()):
+        raise ForbiddenException("not an owner")
+    assert job.status is not JobStatus.running, "must be stopped first"
+    pl = _placements(form)
+    kind = form["template"]
+    command = form.get("command") or "python train.py"
+    master = pl[0]["hostname"]
+    if kind == "torchrun":
+        port = form.get("masterPort") or 29500
+        forms = [launcher.torchrun_task(p["hostname"], p["gpus"], master, port, nnodes=len(pl),
+                                        module=form.get("module") or "tensorhive_fixed_amd.workloads.llama3_ddp")
+                 for p in pl]
+    elif kind == "torch":
+        port = form.get("masterPort") or 29500
+        forms = launcher.pytorch_tcp_tasks([(p["hostname"], g) for p in pl for g in p["gpus"]], master, port, command)
+    elif kind == "tf2":
+        forms = launcher.tf2_tasks([(p["hostname"], p["role"], p["gpus"][0] if p["gpus"] else 0) for p in pl],
+                                   form.get("masterPort") or 2222, command)
+    elif kind == "tf1":
+        forms = launcher.tf1_tasks([p["hostname"] for p in pl if p["role"] == "ps"],
+                                   [(p["hostname"], p["gpus"][0] if p["gpus"] else 0) for p in pl if p["role"] != "ps"],
+                                   form.get("masterPort") or 2222, command)
+    else:
+        raise AssertionError(f"unknown template {kind!r}")
+    created = []
+    for f in forms:
+        body, status = task_ctl.business_create(f, id)
+        assert status == 201, body.get("msg")
+        created.append(body["task"])
+    _wake("job")
+    return {"msg": M("task.create.success"), "tasks": created}, 201
+
+
 def get_templates():
     """Launch templates for the task creator (PyTorch-ROCm torchrun, TF_CONFIG, ClusterSpec)."""
     from ..core.launcher import TEMPLATES

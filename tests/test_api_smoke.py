@@ -127,3 +127,37 @@ def test_per_host_sample_age_header(client, daemon, new_admin, auth_headers):
     ages = dict(kv.rsplit("=", 1) for kv in r.headers["X-Host-Sample-Age-Ms"].split(","))
     assert int(ages["node-a"]) < 5000 and 59000 <= int(ages["node-b"]) < 70000
     assert int(r.headers["X-Sample-Age-Ms"]) >= 59000  # the oldest host
+
+
+def test_generate_distributed_tasks(client, new_user, new_user_2, auth_headers):
+    import json as _json
+
+    from tensorhive_fixed_amd.models.orm import Job, Task
+
+    job = Job(name="dist", description="", user_id=new_user.id)
+    job.save()
+    url = f"/jobs/{job.id}/tasks/generate"
+    st, _ = api(client, "post", url, auth_headers(new_user_2), {"template": "torch", "placements": [{"hostname": "a"}]})
+    assert st == 403
+    st, data = api(client, "post", url, auth_headers(new_user),
+                   {"template": "tf2", "command": "python tf.py",
+                    "placements": [{"hostname": "node-a", "gpu": 0, "role": "chief"},
+                                   {"hostname": "node-a", "gpu": 1, "role": "worker"},
+                                   {"hostname": "node-b", "gpu": 0, "role": "worker"}]})
+    assert st == 201, data
+    tasks = [Task.get(t["id"]) for t in data["tasks"]]
+    cfgs = [_json.loads(dict(t.envs())["TF_CONFIG"]) for t in tasks]
+    assert cfgs[0]["cluster"] == {"chief": ["node-a:2222"], "worker": ["node-a:2223", "node-b:2222"]}
+    assert [c["task"] for c in cfgs] == [{"type": "chief", "index": 0}, {"type": "worker", "index": 0},
+                                         {"type": "worker", "index": 1}]
+    assert [t.gpu_id for t in tasks] == [0, 1, 0]
+    st, data = api(client, "post", url, auth_headers(new_user),
+                   {"template": "torchrun", "placements": [{"hostname": "node-a", "gpus": [0, 1, 2, 3]},
+                                                           {"hostname": "node-b", "gpus": [4, 5, 6, 7]}]})
+    assert st == 201
+    cmds = [Task.get(t["id"]).full_command for t in data["tasks"]]
+    assert cmds[0].startswith("HIP_VISIBLE_DEVICES=0,1,2,3 ") and "--nnodes=2" in cmds[0]
+    assert "--rdzv_endpoint=node-a:29500" in cmds[1] and "--nproc_per_node=4" in cmds[1]
+    assert len(Job.get(job.id).tasks) == 5
+    st, _ = api(client, "post", url, auth_headers(new_user), {"template": "mpi", "placements": [{"hostname": "a"}]})
+    assert st == 422
