@@ -10,11 +10,15 @@ Contract: the returned mean loss must be back-propagated with an upstream gradie
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
 from .linear import _DGRAD_NT
 from .transpose import transpose
+
+_HEAD_NT = os.environ.get("TH_HEAD_WGRAD_NT", "1") == "1"  # +0.3 % step (A/B in profiles/r01_gemm)
 
 
 def ce_rows_(logits: torch.Tensor, target: torch.Tensor, grad_scale: float,
@@ -66,10 +70,14 @@ class _LinearCE(torch.autograd.Function):
             loss_sum += ce_rows_(logits, t[s0: s0 + chunk], scale, ignore_index).sum()
             torch.mm(logits, w_kn, out=dh[s0: s0 + chunk])
             if mg is not None:
+                # dW += dlogitsᵀ hc; with TH_HEAD_WGRAD_NT both operands are transposed first so the
+                # GEMM runs in the K-contiguous form
+                a_op, b_op = (transpose(logits), transpose(hc).t()) if (_HEAD_NT and h2.is_cuda) else (logits.t(), hc)
                 if i == 0 and first_acc:
-                    torch.mm(logits.t(), hc, out=acc)
+                    torch.mm(a_op, b_op, out=acc)
                 else:
-                    acc.addmm_(logits.t(), hc)
+                    acc.addmm_(a_op, b_op)
+                del a_op, b_op
             else:
                 acc.addmm_(logits.t().float(), hc.float())
             del logits
