@@ -8,7 +8,10 @@ JSON line.  ``value`` is the whole-job tokens/s (all ranks).  Weak scaling: per-
 fixed (micro_batch x seq_len tokens per GPU per step).
 
 Each timed step is the full training step: forward, backward with bucketed RCCL gradient
-all-reduce over xGMI, and the fused AdamW update of all 8.03e9 parameters.
+collectives over xGMI, and the fused AdamW update of all 8.03e9 parameters.  With N > 1 the
+optimizer is ZeRO-1 sharded by default (gradient reduce-scatter during backward, each rank
+updates 1/N of the parameters, bf16 all-gather overlapped with the next forward); ``--zero 0``
+selects the replicated all-reduce optimizer.
 Data: synthetic random tokens; weights: random init (no network, no checkpoints).
 """
 from __future__ import annotations
@@ -36,6 +39,7 @@ def main() -> int:
     ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("TH_BENCH_MB", "8")))
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("TH_BENCH_BUCKET_MB", "256")))
     ap.add_argument("--grad-accum", type=int, default=int(os.environ.get("TH_BENCH_ACCUM", "1")))
+    ap.add_argument("--zero", type=int, default=None, help="1 = sharded optimizer (default for N > 1), 0 = replicated")
     args = ap.parse_args()
 
     os.environ.setdefault("PYTORCH_ALLOC_CONF", "expandable_segments:True")  # no fragmentation near the HBM limit
@@ -53,7 +57,8 @@ def main() -> int:
     if info.world != args.gpus and info.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {info.world}", file=sys.stderr)
     cfg = LlamaConfig.named(args.model)
-    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb)
+    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb,
+                 zero=args.zero)
     res = run_timed(tr, args.steps, args.warmup)
     n = info.world
     flops = cfg.flops_per_token(args.seq_len) * res["tokens_per_sec"]
@@ -78,7 +83,9 @@ def main() -> int:
             "seq_len": args.seq_len,
             "tokens_per_gpu_per_step": args.micro_batch * args.grad_accum * args.seq_len,
             "parallelism": f"dp{n}",
-            "optimizer": "AdamW (fp32 master, fused flat kernel, clip 1.0)",
+            "optimizer": "AdamW (fp32 master, fused flat kernel, clip 1.0)"
+                         + (f", ZeRO-1 sharded over {n} ranks" if tr.store.sharded else ""),
+            "zero": 1 if tr.store.sharded else 0,
             "attention": attention_backend(),
             "grad_bucket_mb": args.bucket_mb,
         },

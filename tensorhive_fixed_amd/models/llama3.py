@@ -126,6 +126,9 @@ class Llama(nn.Module):
         self.layers = nn.ModuleList([LlamaBlock(cfg, device, dtype) for _ in range(cfg.n_layers)])
         self.norm = nn.Parameter(torch.ones(cfg.dim, device=device, dtype=dtype))
         self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.dim, device=device, dtype=dtype))
+        # ZeRO-1 hook: called with the parameters about to be read, so a sharded store can make the
+        # stream wait for exactly the all-gather buckets holding them (parallel/flat.py)
+        self.param_gate = None
         self.reset_parameters(seed)
 
     @torch.no_grad()
@@ -155,9 +158,16 @@ class Llama(nn.Module):
 
     def hidden(self, tokens: torch.Tensor) -> torch.Tensor:
         B, S = tokens.shape
+        gate = self.param_gate
+        if gate is not None:
+            gate(self.tok_emb)
         x = embedding(tokens, self.tok_emb).view(B * S, self.cfg.dim)
         for blk in self.layers:
+            if gate is not None:
+                gate(blk.attn_norm, blk.wqkv, blk.wo, blk.ffn_norm, blk.w13, blk.w2)
             x = blk(x, B, S)
+        if gate is not None:
+            gate(self.norm, self.lm_head)
         return rmsnorm(x, self.norm, self.cfg.norm_eps)
 
     def forward(self, tokens: torch.Tensor, targets: torch.Tensor | None = None,

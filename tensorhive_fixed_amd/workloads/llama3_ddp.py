@@ -6,8 +6,10 @@ tensorhive_fixed_amd.workloads.llama3_ddp``), typically by the tensorhive job qu
 ``[th-train] step=… tokens/s=…`` lines which the daemon's log parser turns into the tokens/s
 reported on the dashboard and in BASELINE.md.
 
-One step = forward + backward (gradient buckets all-reduced over RCCL while backward runs) +
-fused flat AdamW with on-device global-norm clipping.  Nothing is skipped inside a step.
+One step = forward + backward (gradient buckets all-reduced -- or, with the ZeRO-1 sharded
+optimizer that is the default for world > 1, reduce-scattered -- over RCCL while backward runs) +
+fused flat AdamW with on-device global-norm clipping (+ the overlapped parameter all-gather when
+sharded).  Nothing is skipped inside a step.
 """
 from __future__ import annotations
 
@@ -61,14 +63,28 @@ class _Range:
             torch.cuda.nvtx.range_pop()
 
 
+def default_zero(world: int) -> int:
+    """ZeRO stage of the payload: 1 (sharded optimizer) whenever there is more than one rank,
+    unless ``TH_ZERO=0`` asks for the replicated DDP optimizer."""
+    env = os.environ.get("TH_ZERO")
+    if env is not None:
+        return int(env)
+    return 1 if world > 1 else 0
+
+
 class Trainer:
     def __init__(self, cfg: LlamaConfig, info: DistInfo, micro_batch: int, seq_len: int,
-                 grad_accum: int = 1, lr: float = 3e-4, bucket_mb: float = 256.0, seed: int = 0):
+                 grad_accum: int = 1, lr: float = 3e-4, bucket_mb: float = 256.0, seed: int = 0,
+                 zero: int | None = None):
         self.cfg, self.info = cfg, info
         self.micro_batch, self.seq_len, self.grad_accum = micro_batch, seq_len, grad_accum
         dev = info.device
+        self.zero = default_zero(info.world) if zero is None else zero
         self.model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
-        self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb)
+        self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb,
+                                    shard=self.zero >= 1 and info.world > 1)
+        if self.store.sharded:
+            self.model.param_gate = self.store.wait_params
         self.opt = FlatAdamW(self.store, lr=lr)
         self.data = SyntheticTokens(cfg.vocab_size, micro_batch, seq_len, dev, info.rank)
         self.tokens_per_step = micro_batch * seq_len * grad_accum  # per rank
@@ -93,29 +109,55 @@ class Trainer:
         return loss_acc
 
     # ------------------------------------------------------------------ checkpoint / resume
+    def _optim_state(self) -> dict:
+        return {"master": self.opt.master, "exp_avg": self.opt.exp_avg, "exp_avg_sq": self.opt.exp_avg_sq}
+
     def state(self) -> dict:
-        """Everything a bit-exact resume needs: flat params, f32 master / moments, step, data RNG."""
-        return {"param_buf": self.store.param_buf, "master": self.opt.master, "exp_avg": self.opt.exp_avg,
-                "exp_avg_sq": self.opt.exp_avg_sq, "step": torch.tensor(self.opt.step_count),
-                "data_drawn": torch.tensor(self.data.drawn), "names": "\n".join(self.store.names)}
+        """Everything a bit-exact resume needs: flat params, f32 master / moments, step, data RNG.
+        With a sharded optimizer the moments are this rank's slices (see :meth:`save`)."""
+        self.store.wait_all_params()
+        st = {"param_buf": self.store.param_buf, "step": torch.tensor(self.opt.step_count),
+              "data_drawn": torch.tensor(self.data.drawn), "names": "\n".join(self.store.names),
+              "zero_world": torch.tensor(self.info.world if self.store.sharded else 0)}
+        if not self.store.sharded:
+            st.update(self._optim_state())
+        return st
+
+    @staticmethod
+    def shard_path(path: str, rank: int, world: int) -> str:
+        return f"{path}.optim.{rank}-of-{world}"
+
+    @staticmethod
+    def _write(obj: dict, path: str) -> None:
+        tmp = path + ".tmp"
+        torch.save({k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in obj.items()}, tmp)
+        os.replace(tmp, path)
 
     def save(self, path: str) -> None:
-        """Rank 0 writes (replicas are identical under DDP); atomic rename."""
-        if self.info.rank != 0:
-            return
-        tmp = path + ".tmp"
-        torch.save({k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in self.state().items()}, tmp)
-        os.replace(tmp, path)
+        """Rank 0 writes the parameters (replicas are identical); with the sharded optimizer every
+        rank also writes its own optimizer slices next to it.  Atomic renames."""
+        st = self.state()
+        if self.store.sharded:
+            self._write(self._optim_state(), self.shard_path(path, self.info.rank, self.info.world))
+        if self.info.rank == 0:
+            self._write(st, path)
 
     def load(self, path: str) -> None:
         st = torch.load(path, map_location="cpu", weights_only=True)
         if st["names"] != "\n".join(self.store.names):
             raise ValueError("checkpoint does not match this model's parameter layout")
+        zero_world = int(st.get("zero_world", torch.tensor(0)))
+        want = self.info.world if self.store.sharded else 0
+        if zero_world != want:
+            raise ValueError(f"checkpoint optimizer sharding ({zero_world} ranks) does not match this run ({want})")
+        opt = st if not self.store.sharded else torch.load(
+            self.shard_path(path, self.info.rank, self.info.world), map_location="cpu", weights_only=True)
         with torch.no_grad():
+            self.store.wait_all_params()
             self.store.param_buf.copy_(st["param_buf"])
-            self.opt.master.copy_(st["master"])
-            self.opt.exp_avg.copy_(st["exp_avg"])
-            self.opt.exp_avg_sq.copy_(st["exp_avg_sq"])
+            self.opt.master.copy_(opt["master"])
+            self.opt.exp_avg.copy_(opt["exp_avg"])
+            self.opt.exp_avg_sq.copy_(opt["exp_avg_sq"])
         self.opt.step_count = int(st["step"])
         # every rank has its own data stream: replay the same number of draws on each
         self.data.skip(int(st["data_drawn"]) - self.data.drawn)
@@ -162,13 +204,15 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--zero", type=int, default=None, help="1: shard the optimizer (default when world > 1)")
     ap.add_argument("--ckpt-dir", default=None, help="write <dir>/ckpt.pt every --ckpt-every steps (rank 0)")
     ap.add_argument("--ckpt-every", type=int, default=0)
     ap.add_argument("--resume", action="store_true", help="continue from <ckpt-dir>/ckpt.pt if present")
     args = ap.parse_args(argv)
     info = init_distributed()
     cfg = LlamaConfig.named(args.model)
-    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb)
+    tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb,
+                 zero=args.zero)
     ckpt = os.path.join(args.ckpt_dir, "ckpt.pt") if args.ckpt_dir else None
     if ckpt and args.resume and os.path.exists(ckpt):
         tr.load(ckpt)

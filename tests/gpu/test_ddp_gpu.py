@@ -25,3 +25,6 @@ def test_two_ranks_stay_identical():
     assert r.returncode == 0, r.stderr[-3000:]
     doc = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert doc["world"] == 2 and doc["params_identical"] and doc["n_buckets"] > 1
+    # ZeRO-1: replicas identical after the all-gathers, same trajectory as the replicated optimizer
+    assert doc["params_identical_zero1"] and doc["zero1_vs_zero0_frac_off"] < 1e-3
+    assert doc["opt_state_numel"][1] < doc["opt_state_numel"][0]

@@ -31,5 +31,6 @@ def test_two_rank_bench_prints_one_json_line(tmp_path):
     assert KEYS <= set(d)
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    assert d["config"]["zero"] == 1  # sharded optimizer is the multi-rank default
     # whole-job aggregate: tokens of both ranks over the (max-over-ranks) step time
     assert abs(d["value"] - 2 * 2 * 64 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
