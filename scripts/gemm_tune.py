@@ -6,9 +6,10 @@
     python scripts/gemm_tune.py resume            # tune only the shapes missing from the table
     python scripts/gemm_tune.py check             # survey again with the tuned table loaded (tuning off)
 
-The GEMMs are exactly the ones the payload issues (ops/linear.py, ops/cross_entropy.py):
-forward ``x @ W^T`` (addmm with the residual for wo / w2), input grad ``dy @ W`` and weight grad
-``dy^T @ x`` written into the flat gradient buffer.
+The GEMMs are exactly the ones the payload issues (ops/linear.py, ops/mlp.py, ops/cross_entropy.py):
+forward ``x @ W^T`` (addmm with the residual for wo / w2), input grad ``dy @ (W^T)^T`` on the
+transposed weight copy (K-contiguous form), weight grad ``dy^T @ x`` written into the flat gradient
+buffer -- for the gate|up projection on transposed operands ``(dy^T) @ (x^T)^T``.
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ import torch
 ROOT = Path(__file__).resolve().parent.parent
 TUNED = ROOT / "tensorhive_fixed_amd" / "ops" / "tuned" / "gemm_gfx950.csv"
 
-T = 16384  # tokens per micro-step (4 x 4096)
+T = int(os.environ.get("TH_TUNE_TOKENS", "32768"))  # tokens per micro-step (bench default MB 8 x 4096)
 D, HQKV, FF, V = 4096, 6144, 14336, 128256
 CH = 4096  # CE chunk
 
@@ -42,16 +43,24 @@ def shapes():
     return out
 
 
-def make(kind, M, N, K, res, dev):
+def make(kind, M, N, K, res, dev, name=""):
     g = torch.Generator(device=dev).manual_seed(0)
     r = lambda *s: torch.randn(*s, device=dev, dtype=torch.bfloat16, generator=g)  # noqa: E731
     if kind == "fwd":  # x[M,K] @ W[N,K]^T
         x, w = r(M, K), r(N, K)
         c = r(M, N) if res else None
         return (lambda: torch.addmm(c, x, w.t())) if res else (lambda: torch.mm(x, w.t()))
-    if kind == "dgrad":  # dy[M,K'] @ W[K',N]   (W stored [out, in] = [K, N])
-        dy, w = r(M, K), r(K, N)
-        return lambda: torch.mm(dy, w)
+    if kind == "dgrad":
+        dy = r(M, K)
+        if name == "head":  # dlogits[M,V] @ W[V,D]
+            w = r(K, N)
+            return lambda: torch.mm(dy, w)
+        wT = r(N, K)  # the transposed weight copy [in, out]: dy @ (W^T)^T, both operands K-contiguous
+        return lambda: torch.mm(dy, wT.t())
+    if name == "w13":  # dW = (dy^T)[N_out, T] @ (x^T)[K_in, T]^T
+        dyT, xT = r(M, K), r(N, K)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        return lambda: torch.mm(dyT, xT.t(), out=out)
     # wgrad: dy^T[N_out, T] @ x[T, K_in] -> out [M=N_out, N=K_in]
     dy, x = r(K, M), r(K, N)
     out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -78,7 +87,7 @@ def survey(tag):
     tot_ms, tot_fl = 0.0, 0.0
     rows = []
     for name, kind, M, N, K, res in shapes():
-        fn = make(kind, M, N, K, res, dev)
+        fn = make(kind, M, N, K, res, dev, name)
         ms = timeit(fn)
         fl = 2.0 * M * N * K
         per_step = 32 if name != "head" else T // CH
