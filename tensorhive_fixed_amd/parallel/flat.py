@@ -191,15 +191,19 @@ class FlatParamStore:
             return [(0, self.numel)] if self.numel else []
         return [b.shard(self.rank, self.world) for b in self.buckets]
 
-    def start_param_gather(self) -> None:
-        """After the optimizer updated the owned slices: all-gather every bucket in place,
-        asynchronously, in forward order (the last bucket holds the embedding and the norms)."""
+    def gather_bucket(self, index: int) -> None:
+        """All-gather bucket ``index`` in place, asynchronously (after its slice was updated)."""
         if not self.sharded or self.world == 1:
             return
+        b = self.buckets[index]
+        lo, hi = b.shard(self.rank, self.world)
+        b.gather = dist.all_gather_into_tensor(self.param_buf[b.start: b.end], self.param_buf[lo:hi],
+                                               group=self.pg, async_op=True)
+
+    def start_param_gather(self) -> None:
+        """All-gather every bucket, in forward order (the last bucket holds the embedding/norms)."""
         for b in reversed(self.buckets):
-            lo, hi = b.shard(self.rank, self.world)
-            b.gather = dist.all_gather_into_tensor(self.param_buf[b.start: b.end], self.param_buf[lo:hi],
-                                                   group=self.pg, async_op=True)
+            self.gather_bucket(b.index)
 
     def wait_params(self, *params: torch.Tensor) -> None:
         """Make the current stream wait for the all-gather of the buckets holding ``params``."""
@@ -232,11 +236,17 @@ class FlatAdamW:
         # (flat_lo, flat_hi, local_lo, weight_decay) segments: owned ranges split at the decay boundary
         self.segments: list[tuple[int, int, int, float]] = []
         local = 0
+        # segment indices per bucket, so the sharded step can hand each bucket to its all-gather
+        # as soon as its slice is updated
+        self.bucket_segments: list[list[int]] = []
         for lo, hi in store.owned_ranges():
+            mine = []
             for a, b, wd in ((lo, min(hi, store.decay_numel), weight_decay), (max(lo, store.decay_numel), hi, 0.0)):
                 if b > a:
+                    mine.append(len(self.segments))
                     self.segments.append((a, b, local, wd))
                     local += b - a
+            self.bucket_segments.append(mine)
         self.local_numel = local
         self.master = torch.empty(local, device=store.device, dtype=torch.float32)
         for a, b, l0, _ in self.segments:
@@ -258,13 +268,18 @@ class FlatAdamW:
                 self.norm_sq.zero_()
             if st.sharded and st.world > 1:
                 dist.all_reduce(self.norm_sq, op=dist.ReduceOp.SUM, group=st.pg)
-        for a, b, l0, wd in self.segments:
-            l1 = l0 + (b - a)
-            adamw_flat_(st.param_buf[a:b], self.master[l0:l1], self.exp_avg[l0:l1], self.exp_avg_sq[l0:l1],
-                        st.grad_buf[a:b], lr=lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
-                        weight_decay=wd, step=self.step_count, grad_scale=scale,
-                        norm_sq=self.norm_sq if self.clip > 0 else None, clip=self.clip)
-        st.start_param_gather()
+        # forward order (last bucket first): in sharded mode each bucket's all-gather starts right after
+        # its slice is updated, overlapping the remaining AdamW launches and then the next forward
+        for bi in reversed(range(len(self.bucket_segments))):
+            for si in self.bucket_segments[bi]:
+                a, b, l0, wd = self.segments[si]
+                l1 = l0 + (b - a)
+                adamw_flat_(st.param_buf[a:b], self.master[l0:l1], self.exp_avg[l0:l1], self.exp_avg_sq[l0:l1],
+                            st.grad_buf[a:b], lr=lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
+                            weight_decay=wd, step=self.step_count, grad_scale=scale,
+                            norm_sq=self.norm_sq if self.clip > 0 else None, clip=self.clip)
+            if st.sharded:
+                st.gather_bucket(bi)
 
     def grad_norm(self) -> float:
         """Global gradient norm of the last step (forces a host sync; for logging only)."""
