@@ -1,0 +1,393 @@
+// Weight-gradient GEMM in the layout training produces, for gfx950 (MI355X):
+//
+//     C[M][N] (+)= sum_k A[k][M] * B[k][N]        (dW = dY^T X, k = tokens)
+//
+// A = dY [tokens][out] and B = X [tokens][in] are both row-major with the reduction index as
+// the SLOW dimension.  hipBLASLt runs this "TN" form at 1.0-1.2 PFLOP/s on the Llama-3-8B
+// shapes against 1.4-1.6 for the K-contiguous forms (profiles/r01_gemm/); the K-contiguous form
+// needs two transposes of activation-sized operands first.  This kernel reads the operands as
+// they are: tiles are staged k-row by k-row with LDS-DMA (global_load_lds_dwordx4) and the MFMA
+// operands are gathered column-wise with the hardware transpose read ds_read_b64_tr_b16.
+//
+//   * tile 256 x 256 x 64, 512 threads = 8 waves as 2 (M) x 4 (N), wave tile 128 x 64,
+//     v_mfma_f32_32x32x16_bf16, 128 f32 accumulators per lane;
+//   * LDS: per stage an A and a B image of 64 k-rows x 512 B; two stages = 128 KB, one
+//     workgroup per CU.  Rows are XOR-swizzled in 64-B chunks by (row & 3) -- applied to the
+//     per-lane GLOBAL source address because LDS-DMA writes lane-linearly -- which makes every
+//     32-lane half of a transposed read (4 k-rows x 64 B) hit 4 distinct chunks of the 256-B bank
+//     row: conflict-free;
+//   * pipeline: the DMA of tile t+1 is in flight while tile t is computed; the wait is a counted
+//     `s_waitcnt vmcnt(8)` (never 0 inside the loop) + raw s_barrier, so the prefetch survives
+//     the barrier (guide §5 "Pipelining across barriers");
+//   * XCD-aware grouped tile order: each XCD (own 4 MB L2) works on a compact 8-row band of
+//     output tiles so A/B k-panels are re-read from its L2;
+//   * optional split-K for grids that would leave CUs idle (f32 slabs + a reduce kernel that
+//     also performs the optional C += accumulation and the bf16 conversion).
+#include "th_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+#define LDS_AS __attribute__((address_space(3)))
+
+namespace {
+constexpr int TM = 256, TN = 256, TK = 64;
+constexpr int NTHR = 512;
+constexpr int ROWB = TN * 2;              // bytes per LDS k-row (TM == TN)
+constexpr int OPB = TK * ROWB;            // 32 KB per operand image
+constexpr int STAGEB = 2 * OPB;           // A + B
+constexpr int LDSB = 2 * STAGEB;          // two stages = 128 KB
+constexpr int GLDS_PER_OP = OPB / (NTHR * 16);  // 4 DMA instructions per lane per operand per stage
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// One 16-B LDS-DMA piece: lane-linear destination (wave-uniform LDS byte address `lds` in M0,
+// + 16*lane), source = wave-uniform 64-bit base (SGPRs) + per-lane 32-bit byte offset.  Issued
+// through inline asm on purpose: for the builtin, hipcc cannot tell which LDS bytes a DMA writes
+// and puts `s_waitcnt vmcnt(0)` in front of every later ds_read, which drains the prefetch each
+// k-tile.  The waits are placed by hand instead (counted vmcnt + s_barrier).
+__device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
+}
+
+__device__ __forceinline__ bf16x8 tr_pair(const char LDS_AS* p0, const char LDS_AS* p1) {
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)p0);
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)p1);
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Stage k-rows [k0, k0+64) of a [K][ld] operand, columns [c0, c0+256), into a lane-linear LDS
+// image whose (row, 64-B chunk c) holds global chunk c ^ (row & 3).  Wave-instruction u writes LDS
+// bytes [u*1KB, +1KB) = rows 2u, 2u+1; a lane's byte offset from the wave-uniform row base depends
+// on u only through the parity of u (row & 3 = (2(u&1) + (lane>>5)) & 3): two VGPRs per operand.
+struct LaneOffs {
+  unsigned o[2];
+};
+__device__ __forceinline__ LaneOffs lane_offs(long ld, long c0, int lane) {
+  LaneOffs r;
+  const int hi = lane >> 5, slot = lane & 31;
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int chunk = (slot >> 2) ^ ((2 * par + hi) & 3);
+    r.o[par] = (unsigned)(2 * ((long)hi * ld + c0 + chunk * 32 + (slot & 3) * 8));
+  }
+  return r;
+}
+__device__ __forceinline__ void stage_op(const ushort* __restrict__ g, const LaneOffs& lo, long ld, long k0,
+                                         unsigned img, int w, int nw) {
+  // nw waves share the 32 wave-instructions of one operand image (8: all waves; 4: one group)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (nw == 8 && j == 1) continue;
+      const int u = i * 8 + w + 4 * j;  // nw == 4: waves w and w+4's pieces
+      const ushort* base = g + (k0 + 2 * u) * ld;
+      glds16(base, lo.o[u & 1], img + u * 1024);
+    }
+  }
+}
+}  // namespace
+
+template <bool SPLIT>
+__global__ __launch_bounds__(NTHR, 1) void gemm_tn_kernel(
+    const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
+    int beta) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[LDSB];
+  char LDS_AS* smem = (char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = SPLIT ? L / splitk : L;
+  const int split = SPLIT ? L % splitk : 0;
+  // grouped order: bands of GM tile-rows, walked column-major inside a band
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = tile / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = tile % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;        // wave tile: rows wm*128, cols wn*64
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int kper = K / splitk;
+  const long kbeg = (long)split * kper;
+  const int nt = kper / TK;
+
+  // transposed-read lane geometry: group g = lane>>4 (h = g>>1 picks k 0-7 / 8-15 of a k-step,
+  // g&1 picks the 16-column half of a 32-column block); lane 4q+p addresses row q, cols 4p..4p+3
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lane_base = (8 * (g >> 1) + q) * ROWB + 32 * (g & 1) + 8 * p;
+  int a_off[4], b_off[2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) a_off[mb] = lane_base + ((((wm * 128 + 32 * mb) >> 5) ^ q) << 6);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) b_off[nb] = lane_base + ((((wn * 64 + 32 * nb) >> 5) ^ q) << 6);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
+
+  // prologue: tiles 0 and 1 in flight
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;  // LDS byte address of the staging array
+  const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
+  stage_op(A, pa, lda, kbeg, lds0, w, 8);
+  stage_op(B, pb, ldb, kbeg, lds0 + OPB, w, 8);
+  if (nt > 1) {
+    stage_op(A, pa, lda, kbeg + TK, lds0 + STAGEB, w, 8);
+    stage_op(B, pb, ldb, kbeg + TK, lds0 + STAGEB + OPB, w, 8);
+  }
+
+  for (int t = 0; t < nt; ++t) {
+    // tile t landed (this wave's DMAs), tile t+1 may stay in flight; the barrier publishes all waves'
+    // (wait + barrier in ONE asm statement with a memory clobber: no LDS read can be scheduled
+    // between them, or above them)
+    if (t + 1 < nt) {
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const char LDS_AS* sa = smem + (t & 1) * STAGEB;
+    const char LDS_AS* sb = sa + OPB;
+#pragma unroll
+    for (int ks = 0; ks < TK / 16; ++ks) {
+      const int ko = ks * 16 * ROWB;  // k-step: rows 16ks .. 16ks+15
+      bf16x8 af[4], bf[2];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[mb] = tr_pair(sa + a_off[mb] + ko, sa + a_off[mb] + ko + 4 * ROWB);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) bf[nb] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb], bf[nb], acc[mb][nb]);
+    }
+    // every wave finished reading this stage before anyone restages it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 2 < nt) {
+      const unsigned dst = lds0 + (t & 1) * STAGEB;
+      stage_op(A, pa, lda, kbeg + (long)(t + 2) * TK, dst, w, 8);
+      stage_op(B, pb, ldb, kbeg + (long)(t + 2) * TK, dst + OPB, w, 8);
+    }
+  }
+
+  // epilogue: D[m][n] of block (mb, nb): n = col on the lane, m = accumulator row
+  const int c32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const long n = n0 + wn * 64 + 32 * nb + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (SPLIT) {
+          slab[((long)split * M + m) * N + n] = acc[mb][nb][r];
+        } else {
+          float v = acc[mb][nb][r];
+          if (beta) v += bf2f(C[m * ldc + n]);
+          C[m * ldc + n] = f2bf(v);
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ping-pong variant: the two wave groups (waves 0-3 = G0: rows 0-127 of the tile, waves 4-7 =
+// G1: rows 128-255; each SIMD hosts one wave of each group) alternate roles every slot:
+//   slot 2t   : G0 gathers ALL its fragments of k-tile t into registers (48 tr reads) and issues
+//               the LDS-DMA of k-tile t+1;       G1 runs its 32 MFMAs of k-tile t-1
+//   slot 2t+1 : G0 runs its 32 MFMAs of k-tile t; G1 gathers its fragments of k-tile t
+// so each SIMD's matrix pipe is fed by one wave while its partner waits on LDS, instead of both
+// waves stalling on the same barrier and the same LDS latency.  Slots end with a workgroup
+// barrier; G1 enters one slot late (an extra barrier at the start, G0 one at the end).
+//   * buffer reuse: k-tile t+1's DMA (slot 2t) overwrites the stage k-tile t-1 used; its last
+//     reader (G1, slot 2t-1) retired its reads (lgkmcnt(0)) before that slot's barrier;
+//   * visibility: G0 waits vmcnt(0) at the end of slot 2t+1, so k-tile t+1 is complete before the
+//     barrier that opens slot 2t+2 (G0 reads) and slot 2t+3 (G1 reads).
+template <bool SPLIT>
+__global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp_kernel(
+    const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
+    int beta) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[LDSB];
+  char LDS_AS* smem = (char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = SPLIT ? L / splitk : L;
+  const int split = SPLIT ? L % splitk : 0;
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = tile / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = tile % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const bool g1 = __builtin_amdgcn_readfirstlane(w) >= 4;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int kper = K / splitk;
+  const long kbeg = (long)split * kper;
+  const int nt = kper / TK;
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lane_base = (8 * (g >> 1) + q) * ROWB + 32 * (g & 1) + 8 * p;
+  int a_off[4], b_off[2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) a_off[mb] = lane_base + ((((wm * 128 + 32 * mb) >> 5) ^ q) << 6);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) b_off[nb] = lane_base + ((((wn * 64 + 32 * nb) >> 5) ^ q) << 6);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
+
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
+  // prologue: k-tile 0 staged by all 8 waves
+  stage_op(A, pa, lda, kbeg, lds0, w, 8);
+  stage_op(B, pb, ldb, kbeg, lds0 + OPB, w, 8);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (g1) asm volatile("s_barrier" ::: "memory");  // G1 enters one slot late
+
+  bf16x8 af[4][4], bf[2][4];  // [block][k-step]
+  for (int t = 0; t < nt; ++t) {
+    // ---- gather slot
+    if (!g1 && t + 1 < nt) {  // G0 stages k-tile t+1 (4 waves x 16 DMA pieces = 64 KB)
+      const unsigned dst = lds0 + ((t + 1) & 1) * STAGEB;
+      const long kt = kbeg + (long)(t + 1) * TK;
+      stage_op(A, pa, lda, kt, dst, w, 4);
+      stage_op(B, pb, ldb, kt, dst + OPB, w, 4);
+    }
+    const char LDS_AS* sa = smem + (t & 1) * STAGEB;
+    const char LDS_AS* sb = sa + OPB;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int ko = ks * 16 * ROWB;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[mb][ks] = tr_pair(sa + a_off[mb] + ko, sa + a_off[mb] + ko + 4 * ROWB);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // ---- compute slot
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!g1) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_barrier" ::: "memory");
+    }
+  }
+  if (!g1) asm volatile("s_barrier" ::: "memory");  // match G1's extra barrier
+
+  const int c32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const long n = n0 + wn * 64 + 32 * nb + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (SPLIT) {
+          slab[((long)split * M + m) * N + n] = acc[mb][nb][r];
+        } else {
+          float v = acc[mb][nb][r];
+          if (beta) v += bf2f(C[m * ldc + n]);
+          C[m * ldc + n] = f2bf(v);
+        }
+      }
+    }
+}
+
+// C[m][n] (+)= sum over splits of slab[s][m][n], 8 elements per thread
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
+                                                             long ldc, int M, int N, int splitk, int beta) {
+  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total8 = (long)M * N / 8;
+  if (i8 >= total8) return;
+  const long e = i8 * 8;
+  const long m = e / N, n = e % N;
+  float v[8];
+  const float4v* s0 = reinterpret_cast<const float4v*>(slab + e);
+  float4v x0 = s0[0], x1 = s0[1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = x0[j]; v[4 + j] = x1[j]; }
+  for (int s = 1; s < splitk; ++s) {
+    const float4v* sp = reinterpret_cast<const float4v*>(slab + (long)s * M * N + e);
+    x0 = sp[0];
+    x1 = sp[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += x0[j]; v[4 + j] += x1[j]; }
+  }
+  ushort8* cp = reinterpret_cast<ushort8*>(C + m * ldc + n);
+  ushort8 o;
+  if (beta) {
+    const ushort8 c = *cp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] + bf2f(c[j]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+  }
+  *cp = o;
+}
+
+// C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  splitk > 1 needs a
+// workspace of splitk*M*N floats.  Returns -1 for shapes the kernel does not tile.
+// flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop
+extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
+                          int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
+  if (lda < M || ldb < N || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -1;
+  if (splitk > 1 && ws == nullptr) return -1;
+  const long tiles = (long)(M / TM) * (N / TN);
+  const bool pp = flags & 1;
+  if (splitk == 1) {
+    if (pp)
+      gemm_tn_pp_kernel<false><<<(unsigned)tiles, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb,
+                                                                (ushort*)C, ldc, nullptr, M, N, K, 1, beta);
+    else
+      gemm_tn_kernel<false><<<(unsigned)tiles, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb,
+                                                             (ushort*)C, ldc, nullptr, M, N, K, 1, beta);
+  } else {
+    if (pp)
+      gemm_tn_pp_kernel<true><<<(unsigned)(tiles * splitk), NTHR, 0, s>>>(
+          (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, ws, M, N, K, splitk, beta);
+    else
+      gemm_tn_kernel<true><<<(unsigned)(tiles * splitk), NTHR, 0, s>>>(
+          (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, ws, M, N, K, splitk, beta);
+    const long n8 = (long)M * N / 8;
+    splitk_reduce_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(ws, (ushort*)C, ldc, M, N, splitk, beta);
+  }
+  TH_CHECK_LAUNCH();
+}

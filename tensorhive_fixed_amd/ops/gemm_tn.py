@@ -1,0 +1,68 @@
+"""Weight-gradient GEMM ``C (+)= Aᵀ·B`` for operands stored [tokens, features] (``csrc/gemm_tn.hip``).
+
+``dW = dYᵀ X`` sums over tokens, the slow dimension of both activation tensors.  hipBLASLt's kernel
+for that operand layout reaches 1.0-1.2 PFLOP/s on the Llama-3-8B projection shapes; the
+gfx950 kernel stages k-rows with LDS-DMA and reads MFMA operands with the hardware transpose read,
+so no operand is transposed in memory.  Shapes it does not tile (M or N not a multiple of 256,
+K not a multiple of 64 x split) fall back to ``torch.mm``.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _lib
+
+_TILE, _TK = 256, 64
+
+
+def supported(m: int, n: int, k: int, splitk: int = 1) -> bool:
+    return m % _TILE == 0 and n % _TILE == 0 and k % (_TK * splitk) == 0
+
+
+def default_splitk(m: int, n: int, k: int, cus: int = 256) -> int:
+    """Split K when the output tiles leave a ragged last round on the 256 CUs (1 workgroup/CU)."""
+    env = os.environ.get("TH_GEMM_TN_SPLITK")
+    if env:
+        return int(env)
+    tiles = (m // _TILE) * (n // _TILE)
+    best, best_eff = 1, 0.0
+    for s in (1, 2, 3, 4):
+        if not supported(m, n, k, s):
+            continue
+        rounds = -(-tiles * s // cus)
+        eff = tiles * s / (rounds * cus) - 0.03 * (s > 1)  # the slab round trip costs a few percent
+        if eff > best_eff + 1e-9:
+            best, best_eff = s, eff
+    return best
+
+
+_PP = int(os.environ.get("TH_GEMM_TN_PP", "1"))
+
+
+def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+             splitk: int | None = None, pingpong: bool | None = None) -> torch.Tensor:
+    """``out[M, N] (+)= a[K, M]ᵀ @ b[K, N]`` (bf16 in / out, f32 accumulation)."""
+    K, M = a.shape
+    K2, N = b.shape
+    if K2 != K or tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm_tn_: shapes {tuple(a.shape)}, {tuple(b.shape)} -> {tuple(out.shape)}")
+    if not a.is_cuda:
+        r = a.float().t() @ b.float()
+        out.copy_((out.float() + r if accumulate else r).to(out.dtype))
+        return out
+    sk = default_splitk(M, N, K) if splitk is None else splitk
+    ok = (a.dtype == b.dtype == out.dtype == torch.bfloat16 and supported(M, N, K, sk)
+          and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1)
+    if not ok:
+        if accumulate:
+            out.addmm_(a.t(), b)
+        else:
+            torch.mm(a.t(), b, out=out)
+        return out
+    ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
+    _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
+              M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
+              int(_PP if pingpong is None else pingpong), _lib.stream_ptr(a.device))
+    return out
