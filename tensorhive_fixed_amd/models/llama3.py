@@ -81,6 +81,9 @@ class LlamaConfig:
 # projections whose weight grad runs on transposed operand copies (ops/linear.py): where the GEMM
 # speed-up outweighs the transposes (measured: profiles/r01_gemm/)
 WGRAD_NT = set(filter(None, os.environ.get("TH_WGRAD_NT_LAYERS", "w13").split(",")))
+# projections whose weight grad runs on the gfx950 TN kernel (ops/gemm_tn.py), measured faster than
+# hipBLASLt there (scripts/bench_gemm_tn.py)
+WGRAD_TN = set(filter(None, os.environ.get("TH_WGRAD_TN_LAYERS", "wqkv,wo,w2").split(",")))
 _FORK = os.environ.get("TH_RMSNORM_FORK", "1") == "1"
 
 
@@ -107,15 +110,15 @@ class LlamaBlock(nn.Module):
         c = self.cfg
         # rmsnorm_fork: the residual gradient is added inside the RMSNorm backward kernel
         h, x = _norm(x, self.attn_norm, c.norm_eps)
-        qkv = linear(h, self.wqkv, wgrad_nt="wqkv" in WGRAD_NT)
+        qkv = linear(h, self.wqkv, wgrad_nt="wqkv" in WGRAD_NT, wgrad_tn="wqkv" in WGRAD_TN)
         o = qkv_attention(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta)
-        x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT)
+        x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT, wgrad_tn="wo" in WGRAD_TN)
         h, x = _norm(x, self.ffn_norm, c.norm_eps)
         if "w13" in WGRAD_NT:  # fused gate|up + SwiGLU node: transposed dGU from the SwiGLU kernel
             a = gate_up_swiglu(h, self.w13)
         else:
             a = swiglu(linear(h, self.w13))
-        return linear(a, self.w2, residual=x, wgrad_nt="w2" in WGRAD_NT)
+        return linear(a, self.w2, residual=x, wgrad_nt="w2" in WGRAD_NT, wgrad_tn="w2" in WGRAD_TN)
 
 
 class Llama(nn.Module):

@@ -15,10 +15,12 @@ import os
 import torch
 
 from . import _lib
+from .gemm_tn import gemm_tn_, supported as gemm_tn_supported
 from .linear import _DGRAD_NT
 from .transpose import transpose
 
 _HEAD_NT = os.environ.get("TH_HEAD_WGRAD_NT", "1") == "1"  # +0.3 % step (A/B in profiles/r01_gemm)
+_HEAD_TN = os.environ.get("TH_HEAD_WGRAD_TN", "0") == "1"  # gfx950 TN kernel for dW += dlogitsᵀ h
 
 
 def ce_rows_(logits: torch.Tensor, target: torch.Tensor, grad_scale: float,
@@ -72,6 +74,10 @@ class _LinearCE(torch.autograd.Function):
             if mg is not None:
                 # dW += dlogitsᵀ hc; with TH_HEAD_WGRAD_NT both operands are transposed first so the
                 # GEMM runs in the K-contiguous form
+                if _HEAD_TN and h2.is_cuda and gemm_tn_supported(w.shape[0], w.shape[1], hc.shape[0]):
+                    # TN kernel straight from [tokens, V] logits and [tokens, D] hidden states
+                    gemm_tn_(logits, hc, acc, accumulate=not (i == 0 and first_acc))
+                    continue
                 a_op, b_op = (transpose(logits), transpose(hc).t()) if (_HEAD_NT and h2.is_cuda) else (logits.t(), hc)
                 if i == 0 and first_acc:
                     torch.mm(a_op, b_op, out=acc)
