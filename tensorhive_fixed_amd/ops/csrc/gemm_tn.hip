@@ -328,6 +328,150 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong v2: k-tiles of 32 in a 4-stage LDS ring (4 x 32 KB).  The deeper ring lets each group
+// stage its own operand two k-tiles ahead inside its own gather slot -- G0 the A image, G1 the B
+// image -- so the LDS-DMA writes are spread over every slot instead of piling onto one group's
+// gather slot (in the 2-stage schedule the even slots carried 96 KB of reads + 64 KB of DMA).
+//   G0, iteration t: slot 2t   : DMA A(t+2); gather k-tile t       | barrier
+//                    slot 2t+1 : 16 MFMAs of k-tile t; vmcnt -> A(t+1) landed | barrier
+//   G1, iteration t: slot 2t+1 : DMA B(t+2); gather k-tile t; vmcnt -> B(t+1) landed | barrier
+//                    slot 2t+2 : 16 MFMAs of k-tile t          | barrier
+// Stage j%4 is rewritten (tile j+4) only 6 slots after its last reader; each wave's DMAs retire
+// in issue order, so vmcnt(4) (one 4-piece DMA still in flight) retires the older tile.
+constexpr int TK2 = 32;
+constexpr int OPB2 = TK2 * ROWB;        // 16 KB
+constexpr int STAGEB2 = 2 * OPB2;       // 32 KB
+constexpr int NSTAGE2 = 4;
+
+__device__ __forceinline__ void stage_op2(const ushort* __restrict__ g, const LaneOffs& lo, long ld, long k0,
+                                          unsigned img, int w4) {
+  // 16 wave-instructions (32 rows x 512 B) over the 4 waves of one group
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = i * 4 + w4;
+    const ushort* base = g + (k0 + 2 * u) * ld;
+    glds16(base, lo.o[u & 1], img + u * 1024);
+  }
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
+    const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
+    int beta) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[NSTAGE2 * STAGEB2];
+  char LDS_AS* smem = (char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = SPLIT ? L / splitk : L;
+  const int split = SPLIT ? L % splitk : 0;
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = tile / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = tile % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3, w4 = w & 3;
+  const bool g1 = w >= 4;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int kper = K / splitk;
+  const long kbeg = (long)split * kper;
+  const int nt = kper / TK2;
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lane_base = (8 * (g >> 1) + q) * ROWB + 32 * (g & 1) + 8 * p;
+  int a_off[4], b_off[2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) a_off[mb] = lane_base + ((((wm * 128 + 32 * mb) >> 5) ^ q) << 6);
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) b_off[nb] = lane_base + ((((wn * 64 + 32 * nb) >> 5) ^ q) << 6);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
+
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
+  // prologue: k-tiles 0 and 1 (A by G0, B by G1), all landed before the first slot
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j < nt) {
+      if (!g1) stage_op2(A, pa, lda, kbeg + j * TK2, lds0 + j * STAGEB2, w4);
+      else stage_op2(B, pb, ldb, kbeg + j * TK2, lds0 + j * STAGEB2 + OPB2, w4);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (g1) asm volatile("s_barrier" ::: "memory");  // G1 enters one slot late
+
+  bf16x8 af[4][2], bf[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const bool more = t + 2 < nt;
+    // ---- gather slot (+ this group's DMA two k-tiles ahead)
+    if (more) {
+      const unsigned st = lds0 + ((t + 2) & (NSTAGE2 - 1)) * STAGEB2;
+      if (!g1) stage_op2(A, pa, lda, kbeg + (long)(t + 2) * TK2, st, w4);
+      else stage_op2(B, pb, ldb, kbeg + (long)(t + 2) * TK2, st + OPB2, w4);
+    }
+    const char LDS_AS* sa = smem + (t & (NSTAGE2 - 1)) * STAGEB2;
+    const char LDS_AS* sb = sa + OPB2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ko = ks * 16 * ROWB;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[mb][ks] = tr_pair(sa + a_off[mb] + ko, sa + a_off[mb] + ko + 4 * ROWB);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
+    }
+    if (g1) {  // G1's B image of k-tile t+1 must land before G0 gathers it (next slot)
+      if (more) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // ---- compute slot
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!g1) {  // G0's A image of k-tile t+1 landed before the barrier that opens its gather
+      if (more) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_barrier" ::: "memory");
+    }
+  }
+  if (!g1) asm volatile("s_barrier" ::: "memory");
+
+  const int c32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const long n = n0 + wn * 64 + 32 * nb + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (SPLIT) {
+          slab[((long)split * M + m) * N + n] = acc[mb][nb][r];
+        } else {
+          float v = acc[mb][nb][r];
+          if (beta) v += bf2f(C[m * ldc + n]);
+          C[m * ldc + n] = f2bf(v);
+        }
+      }
+    }
+}
+
 // C[m][n] (+)= sum over splits of slab[s][m][n], 8 elements per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
                                                              long ldc, int M, int N, int splitk, int beta) {
@@ -363,31 +507,33 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 // C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  splitk > 1 needs a
 // workspace of splitk*M*N floats.  Returns -1 for shapes the kernel does not tile.
-// flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop
+// flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop;
+//        bit1 = ping-pong v2 (k-tiles of 32, 4-stage ring, per-group DMA; needs K % (32*splitk) == 0)
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
+  const bool pp2 = flags & 2;
   if (lda < M || ldb < N || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -1;
   if (splitk > 1 && ws == nullptr) return -1;
   const long tiles = (long)(M / TM) * (N / TN);
   const bool pp = flags & 1;
-  if (splitk == 1) {
-    if (pp)
-      gemm_tn_pp_kernel<false><<<(unsigned)tiles, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb,
-                                                                (ushort*)C, ldc, nullptr, M, N, K, 1, beta);
-    else
-      gemm_tn_kernel<false><<<(unsigned)tiles, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb,
-                                                             (ushort*)C, ldc, nullptr, M, N, K, 1, beta);
-  } else {
-    if (pp)
-      gemm_tn_pp_kernel<true><<<(unsigned)(tiles * splitk), NTHR, 0, s>>>(
-          (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, ws, M, N, K, splitk, beta);
-    else
-      gemm_tn_kernel<true><<<(unsigned)(tiles * splitk), NTHR, 0, s>>>(
-          (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, ws, M, N, K, splitk, beta);
+  const unsigned grid = (unsigned)(tiles * splitk);
+  const ushort *a = (const ushort*)A, *b = (const ushort*)B;
+  ushort* c = (ushort*)C;
+  float* slab = splitk > 1 ? ws : nullptr;
+#define TH_TN_LAUNCH(KERNEL)                                                                     \
+  do {                                                                                          \
+    if (splitk > 1) KERNEL<true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
+    else KERNEL<false><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
+  } while (0)
+  if (pp2) TH_TN_LAUNCH(gemm_tn_pp2_kernel);
+  else if (pp) TH_TN_LAUNCH(gemm_tn_pp_kernel);
+  else TH_TN_LAUNCH(gemm_tn_kernel);
+#undef TH_TN_LAUNCH
+  if (splitk > 1) {
     const long n8 = (long)M * N / 8;
-    splitk_reduce_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(ws, (ushort*)C, ldc, M, N, splitk, beta);
+    splitk_reduce_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta);
   }
   TH_CHECK_LAUNCH();
 }
