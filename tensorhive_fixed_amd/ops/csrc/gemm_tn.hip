@@ -355,7 +355,17 @@ __device__ __forceinline__ void stage_op2(const ushort* __restrict__ g, const La
   }
 }
 
-template <bool SPLIT>
+// vmcnt(4 * n) with n in 0..2 (immediate operand)
+__device__ __forceinline__ void wait_dma_barrier(int n) {
+  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// AHEAD = how many k-tiles ahead each group's DMA runs (2: two slots of lead time per tile, 3: four;
+// with 3 the stage a DMA overwrites was gathered one slot earlier, so G1 retires its reads
+// (lgkmcnt(0)) before its gather slot ends)
+template <bool SPLIT, int AHEAD>
 __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
     ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
@@ -399,9 +409,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
 
   const unsigned lds0 = (unsigned)(uintptr_t)smem;
   const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
-  // prologue: k-tiles 0 and 1 (A by G0, B by G1), all landed before the first slot
+  // prologue: k-tiles 0 .. AHEAD-1 (A by G0, B by G1), all landed before the first slot
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < AHEAD; ++j) {
     if (j < nt) {
       if (!g1) stage_op2(A, pa, lda, kbeg + j * TK2, lds0 + j * STAGEB2, w4);
       else stage_op2(B, pb, ldb, kbeg + j * TK2, lds0 + j * STAGEB2 + OPB2, w4);
@@ -412,12 +422,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
 
   bf16x8 af[4][2], bf[2][2];
   for (int t = 0; t < nt; ++t) {
-    const bool more = t + 2 < nt;
-    // ---- gather slot (+ this group's DMA two k-tiles ahead)
-    if (more) {
-      const unsigned st = lds0 + ((t + 2) & (NSTAGE2 - 1)) * STAGEB2;
-      if (!g1) stage_op2(A, pa, lda, kbeg + (long)(t + 2) * TK2, st, w4);
-      else stage_op2(B, pb, ldb, kbeg + (long)(t + 2) * TK2, st + OPB2, w4);
+    // DMAs younger than k-tile t+1's that are in flight at the end of this iteration
+    const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
+    // ---- gather slot (+ this group's DMA AHEAD k-tiles ahead)
+    if (t + AHEAD < nt) {
+      const unsigned st = lds0 + ((t + AHEAD) & (NSTAGE2 - 1)) * STAGEB2;
+      if (!g1) stage_op2(A, pa, lda, kbeg + (long)(t + AHEAD) * TK2, st, w4);
+      else stage_op2(B, pb, ldb, kbeg + (long)(t + AHEAD) * TK2, st + OPB2, w4);
     }
     const char LDS_AS* sa = smem + (t & (NSTAGE2 - 1)) * STAGEB2;
     const char LDS_AS* sb = sa + OPB2;
@@ -430,8 +441,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
       for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
     }
     if (g1) {  // G1's B image of k-tile t+1 must land before G0 gathers it (next slot)
-      if (more) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (AHEAD >= 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_dma_barrier(younger);
     } else {
       asm volatile("s_barrier" ::: "memory");
     }
@@ -444,8 +455,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
         for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
     __builtin_amdgcn_sched_barrier(0);
     if (!g1) {  // G0's A image of k-tile t+1 landed before the barrier that opens its gather
-      if (more) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      wait_dma_barrier(younger);
     } else {
       asm volatile("s_barrier" ::: "memory");
     }
@@ -508,7 +518,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  splitk > 1 needs a
 // workspace of splitk*M*N floats.  Returns -1 for shapes the kernel does not tile.
 // flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop;
-//        bit1 = ping-pong v2 (k-tiles of 32, 4-stage ring, per-group DMA; needs K % (32*splitk) == 0)
+//        bit1 = ping-pong v2 (k-tiles of 32, 4-stage ring, per-group DMA two k-tiles ahead);
+//        bit2 (with bit1) = DMA three k-tiles ahead
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -527,10 +538,17 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
     if (splitk > 1) KERNEL<true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
     else KERNEL<false><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
   } while (0)
-  if (pp2) TH_TN_LAUNCH(gemm_tn_pp2_kernel);
+#define TH_TN_LAUNCH2(KERNEL, AH)                                                                \
+  do {                                                                                          \
+    if (splitk > 1) KERNEL<true, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
+    else KERNEL<false, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
+  } while (0)
+  if (pp2 && (flags & 4)) TH_TN_LAUNCH2(gemm_tn_pp2_kernel, 3);
+  else if (pp2) TH_TN_LAUNCH2(gemm_tn_pp2_kernel, 2);
   else if (pp) TH_TN_LAUNCH(gemm_tn_pp_kernel);
   else TH_TN_LAUNCH(gemm_tn_kernel);
 #undef TH_TN_LAUNCH
+#undef TH_TN_LAUNCH2
   if (splitk > 1) {
     const long n8 = (long)M * N / 8;
     splitk_reduce_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta);
