@@ -81,25 +81,29 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // Stage `16*NP` x 128 bf16 rows (global, row stride ld) into registers with 256 threads.
-// Thread t covers row 16*i + 4*(t>>6) + (t&3), 16-byte chunk (t>>2)&15: every 16-lane quarter of a
-// wave then writes 4 rows x 4 chunks, i.e. 16 distinct 16-byte bank slots of the LDS image --
-// conflict-free ds_write_b128 (one row per quarter-wave would be 4-way conflicted).  Rows >= limit
-// are clamped to limit-1 (finite data; the consumers mask those keys), so the loads are
-// unconditional -- no divergent branch per load.
+// Thread t covers row 16*i + 2*((t>>3)&7) + ((t>>2)&1), 16-byte chunk 4*(t>>6) + (t&3).  A
+// ds_write_b128 is serviced in groups of 8 contiguous lanes with banks (a/4) mod 32, i.e. 128 B:
+// each such group writes 2 adjacent rows x 4 chunks = 128 contiguous bytes of the image (the XOR
+// only permutes slots inside a row's 64 B) -> conflict-free.  (A 4-rows x 2-chunks group put rows
+// r and r+2 on the same banks: 2-way, 20-25 % of the kernels' LDS cycles in SQ_LDS_BANK_CONFLICT.)
+// Rows >= limit are clamped to limit-1 (finite data; the consumers mask those keys), so the loads
+// are unconditional -- no divergent branch per load.
+__device__ __forceinline__ int stage_row(int tid) { return 2 * ((tid >> 3) & 7) + ((tid >> 2) & 1); }
+__device__ __forceinline__ int stage_ch(int tid) { return 4 * ((tid >> 6) & 3) + (tid & 3); }
 template <int NP>
 __device__ __forceinline__ void stage_load(ushort8 (&r)[NP], const ushort* base, long ld, int row0,
                                            int limit, int tid) {
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    const int row = min(row0 + 16 * i + 4 * (tid >> 6) + (tid & 3), limit - 1);
-    r[i] = *reinterpret_cast<const ushort8*>(base + (long)row * ld + (((tid >> 2) & 15) << 3));
+    const int row = min(row0 + 16 * i + stage_row(tid), limit - 1);
+    r[i] = *reinterpret_cast<const ushort8*>(base + (long)row * ld + (stage_ch(tid) << 3));
   }
 }
 template <int NP>
 __device__ __forceinline__ void stage_store(char* img, const ushort8 (&r)[NP], int tid) {
 #pragma unroll
   for (int i = 0; i < NP; ++i)
-    *reinterpret_cast<ushort8*>(img + img_off(16 * i + 4 * (tid >> 6) + (tid & 3), (tid >> 2) & 15)) = r[i];
+    *reinterpret_cast<ushort8*>(img + img_off(16 * i + stage_row(tid), stage_ch(tid))) = r[i];
 }
 
 // Logical block -> (batch, q head, q block).  QMAJOR: q blocks heaviest-first across all heads
@@ -483,11 +487,11 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   const ushort* Kb = K + b * bs + (long)hk * HD;
   const ushort* Vb = V + b * bs + (long)hk * HD;
   {
-    // 256 rows x 16 chunks = 4096 chunks per tensor, 8 per thread; a quarter-wave covers
-    // 4 rows x 4 chunks (conflict-free ds_write_b128, see stage_load)
+    // 256 rows x 16 chunks = 4096 chunks per tensor, 8 per thread; every 8-lane write group
+    // covers 2 rows x 4 chunks = 128 contiguous bytes (conflict-free ds_write_b128, see stage_load)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int row = 32 * i + 4 * (tid >> 6) + (tid & 3), ch = (tid >> 2) & 15;
+      const int row = 32 * i + 2 * ((tid >> 3) & 15) + ((tid >> 2) & 1), ch = 4 * (tid >> 7) + (tid & 3);
       const bool ok = kblk0 + row < S;
       const long go = (long)(kblk0 + row) * ld + (ch << 3);
       *reinterpret_cast<ushort8*>(ks + img_off(row, ch)) = ok ? *reinterpret_cast<const ushort8*>(Kb + go) : ushort8(0);
@@ -502,13 +506,17 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   const int qt0 = causal ? kblk0 / B_BQ : 0;
   const int per_head = nqt - qt0;
   const int total = G * per_head;
-  // Q/dO tile: 32 rows x 16 chunks = 512 chunks -> one per thread per tensor (conflict-free map)
-  const int srow = 4 * (tid >> 6) + (tid & 3), sch = (tid >> 2) & 15;
+  // Q/dO tile: 32 rows x 16 chunks = 512 chunks -> one per thread per tensor (conflict-free map:
+  // 8-lane write groups cover 2 rows x 4 chunks)
+  const int srow = 2 * ((tid >> 3) & 15) + ((tid >> 2) & 1), sch = 4 * (tid >> 7) + (tid & 3);
   ushort8 qr, gr;
   float lr = 0.f, dr = 0.f;
-  auto prefetch = [&](int it) {
-    const int hq = hk * G + it / per_head;
-    const int qq0 = (qt0 + it % per_head) * B_BQ;
+  // (head, query tile) of the prefetch and of the current iteration, advanced incrementally (a
+  // runtime division per iteration cost ~80 scalar instructions per wave)
+  int pf_h = 0, pf_t = 0, cur_t = 0;
+  auto prefetch = [&](int h_i, int t_i) {
+    const int hq = hk * G + h_i;
+    const int qq0 = (qt0 + t_i) * B_BQ;
     const bool ok = qq0 + srow < S;
     qr = ok ? *reinterpret_cast<const ushort8*>(Q + b * bs + (long)hq * HD + (long)(qq0 + srow) * ld + (sch << 3)) : ushort8(0);
     gr = ok ? *reinterpret_cast<const ushort8*>(dO + b * bso + (long)hq * HD + (long)(qq0 + srow) * ldo + (sch << 3)) : ushort8(0);
@@ -519,7 +527,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
       dr = qq < S ? Dl[st + qq] : 0.f;
     }
   };
-  if (total > 0) prefetch(0);
+  if (total > 0) prefetch(0, 0);
   int krow = 32 * w + c32;
   // static priority for the second-dispatched half (waves 4-7): it otherwise loses VALU
   // arbitration to its SIMD partner on every segment (guide T5, static form)
@@ -530,8 +538,10 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     *reinterpret_cast<ushort8*>(gs + img_off(srow, sch)) = gr;
     if (tid < B_BQ) { ls[tid] = lr; ds[tid] = dr; }
     __syncthreads();
-    const int qbase = (qt0 + it % per_head) * B_BQ;
-    if (it + 1 < total) prefetch(it + 1);
+    const int qbase = (qt0 + cur_t) * B_BQ;
+    if (++cur_t == per_head) cur_t = 0;
+    if (++pf_t == per_head) { pf_t = 0; ++pf_h; }
+    if (it + 1 < total) prefetch(pf_h, pf_t);
     if (causal && qbase + B_BQ - 1 < k0) continue;  // all queries of the tile precede our keys
     asm volatile("" : "+v"(krow));  // keep the K/V row reads inside the loop (see header)
     f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
