@@ -523,7 +523,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     if (tid < B_BQ) {
       const int qq = qq0 + tid;
       const long st = ((long)b * Hq + hq) * S;
-      lr = qq < S ? LSE[st + qq] * LOG2E : INFINITY;
+      lr = qq < S ? LSE[st + qq] : INFINITY;  // scaled by log2(e) when stored: no use right after the load
       dr = qq < S ? Dl[st + qq] : 0.f;
     }
   };
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     __syncthreads();
     *reinterpret_cast<ushort8*>(qs + img_off(srow, sch)) = qr;
     *reinterpret_cast<ushort8*>(gs + img_off(srow, sch)) = gr;
-    if (tid < B_BQ) { ls[tid] = lr; ds[tid] = dr; }
+    if (tid < B_BQ) { ls[tid] = lr * LOG2E; ds[tid] = dr; }
     __syncthreads();
     const int qbase = (qt0 + cur_t) * B_BQ;
     if (++cur_t == per_head) cur_t = 0;
