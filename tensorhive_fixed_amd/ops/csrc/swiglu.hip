@@ -55,21 +55,34 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const ushort* __restric
 }
 
 // Backward that ALSO writes the transposed gradient dguT[2F, T] (the K-contiguous operand of the
-// gate|up weight-grad GEMM, see ops/linear.py): one 128-token x 64-feature tile per workgroup,
-// gate and up halves staged in LDS (odd-dword pitch) and written out as 256-B row segments.
+// gate|up weight-grad GEMM, see ops/linear.py): one 128-token x 64-feature tile per workgroup.
 // Costs one extra 2F*T*2-byte write instead of a separate transpose pass (read + write).
-constexpr int ST_R = 128, ST_C = 64, ST_P = ST_C + 2;
+//   * dg / du tiles go to LDS as 128-B token rows (ds_write_b128; an 8-lane write group covers one
+//     row: conflict-free) with 16-B chunk c of row r stored at chunk c ^ swz(r);
+//   * the transpose is done by the LDS hardware: ds_read_b64_tr_b16 hands each lane 4 consecutive
+//     tokens of ONE feature, two of them make a 16-B piece of a dguT row.  A wave writes 16
+//     feature rows x 64 contiguous bytes per store instruction;
+//   * swz(r) = 2*(((r>>1)&1) | ((r>>3)&1)<<1) puts the 8 token rows a 32-lane half reads
+//     ({0-3, 8-11} + 16k or {4-7, 12-15} + 16k) on 8 distinct 32-B bank groups: conflict-free.
+// (The previous version gathered the transposed pieces with 64 ds_read_u16 per thread and wrote
+// 16-B pieces 64 B apart: 1.71 ms at T 32768, F 14336.)
+constexpr int ST_R = 128, ST_C = 64;
+
+__device__ __forceinline__ int st_swz(int r) { return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)); }
+__device__ __forceinline__ int st_off(int r, int chunk) { return r * 128 + ((chunk ^ st_swz(r)) << 4); }
+
+typedef short i16x4s __attribute__((ext_vector_type(4)));
+#define ST_LDS __attribute__((address_space(3)))
 
 __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const ushort* __restrict__ dout,
                                                            const ushort* __restrict__ gu,
                                                            ushort* __restrict__ dgu,
                                                            ushort* __restrict__ dguT, long T, int F) {
-  __shared__ ushort tg[ST_R * ST_P];
-  __shared__ ushort tu[ST_R * ST_P];
+  __shared__ __attribute__((aligned(16))) char tile[2 * ST_R * 128];  // [g|u][token][64 features]
   const int tid = threadIdx.x;
   const long ntc = F / ST_C;
   const long r0 = (blockIdx.x / ntc) * ST_R, c0 = (blockIdx.x % ntc) * ST_C;
-  const int lc = (tid & 7) * 8;
+  const int lch = tid & 7, lc = lch * 8;
   ushort8 g[4], u[4], d[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -95,31 +108,32 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const ushort* __restr
       *reinterpret_cast<ushort8*>(dgu + row * 2 * F + c0 + lc) = dg;
       *reinterpret_cast<ushort8*>(dgu + row * 2 * F + F + c0 + lc) = du;
     }
-    unsigned* pg = reinterpret_cast<unsigned*>(tg + lr * ST_P + lc);
-    unsigned* pu = reinterpret_cast<unsigned*>(tu + lr * ST_P + lc);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pg[j] = (unsigned)dg[2 * j] | ((unsigned)dg[2 * j + 1] << 16);
-      pu[j] = (unsigned)du[2 * j] | ((unsigned)du[2 * j + 1] << 16);
-    }
+    *reinterpret_cast<ushort8*>(tile + st_off(lr, lch)) = dg;
+    *reinterpret_cast<ushort8*>(tile + ST_R * 128 + st_off(lr, lch)) = du;
   }
   __syncthreads();
-  // 4 lanes per output row (feature), 32 tokens each
-  const int oc = tid >> 2, orr = (tid & 3) * 32;
-  ushort* og = dguT + (c0 + oc) * T + r0 + orr;
-  ushort* ou = dguT + (F + c0 + oc) * T + r0 + orr;
+  // 2 halves x 4 feature blocks of 16 x 4 token groups of 32 = 32 wave-steps, 8 per wave.  In a
+  // wave-step, 16-lane group grp takes tokens tg0 + 8*grp .. +7 of features fb*16 .. +15.
+  const int lane = tid & 63, w = tid >> 6, grp = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    ushort8 wg, wu;
+  for (int k = 0; k < 8; ++k) {
+    const int step = w * 8 + k;
+    const int half = step >> 4, fb = (step >> 2) & 3, tg0 = (step & 3) * 32;
+    const int rbase = tg0 + 8 * grp;
+    const int col = fb * 16 + 4 * p;  // lane 4q+p: row q, features col .. col+3
+    const char* base = tile + half * ST_R * 128 + ((col & 7) << 1);
+    const int ch = col >> 3;
+    const i16x4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ST_LDS i16x4s*)(base + st_off(rbase + q, ch)));
+    const i16x4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ST_LDS i16x4s*)(base + st_off(rbase + 4 + q, ch)));
+    ushort8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      wg[j] = tg[(orr + 8 * q + j) * ST_P + oc];
-      wu[j] = tu[(orr + 8 * q + j) * ST_P + oc];
+    for (int e = 0; e < 4; ++e) {
+      o[e] = (ushort)lo[e];
+      o[4 + e] = (ushort)hi[e];
     }
-    if (r0 + orr + 8 * q < T) {
-      *reinterpret_cast<ushort8*>(og + 8 * q) = wg;
-      *reinterpret_cast<ushort8*>(ou + 8 * q) = wu;
-    }
+    const long feat = (long)half * F + c0 + fb * 16 + i16;
+    const long tok = r0 + rbase;
+    if (tok < T) *reinterpret_cast<ushort8*>(dguT + feat * T + tok) = o;
   }
 }
 
