@@ -482,6 +482,151 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One wave per SIMD, 128 x 128 per wave (the shape hipBLASLt's fast kernels use on gfx950): 4 waves
+// as 2 (M) x 2 (N), 256 f32 accumulators per lane (the compiler keeps them in AGPRs: a lone wave per
+// SIMD owns the whole 512-entry register file), k-tiles of 32 in the 4-stage ring (DMA two k-tiles
+// ahead, 8 pieces per wave per stage).  Twice the MFMAs per fragment of the 8-wave kernels: the
+// LDS read traffic per FLOP drops by a third.  With no partner wave on the SIMD, latency is hidden
+// inside the wave: the fragments of k-step s+1 are read while the MFMAs of k-step s run, and the
+// k-tile boundary (counted vmcnt + barrier) sits between the two halves of the last k-step's MFMAs
+// so the first reads of the next k-tile overlap 8 MFMAs already issued.
+constexpr int W4_THR = 256;
+
+__device__ __forceinline__ void stage_op_w4(const ushort* __restrict__ g, const LaneOffs& lo, long ld, long k0,
+                                            unsigned img, int w) {
+  // 16 wave-instructions (32 rows x 512 B) over 4 waves
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = i * 4 + w;
+    const ushort* base = g + (k0 + 2 * u) * ld;
+    glds16(base, lo.o[u & 1], img + u * 1024);
+  }
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(W4_THR, 1) void gemm_tn_w4_kernel(
+    const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
+    int beta) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[NSTAGE2 * STAGEB2];
+  char LDS_AS* smem = (char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = SPLIT ? L / splitk : L;
+  const int split = SPLIT ? L % splitk : 0;
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = tile / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = tile % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;  // wave tile: rows wm*128, cols wn*128
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int kper = K / splitk;
+  const long kbeg = (long)split * kper;
+  const int nt = kper / TK2;
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lane_base = (8 * (g >> 1) + q) * ROWB + 32 * (g & 1) + 8 * p;
+  int a_off[4], b_off[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a_off[j] = lane_base + ((((wm * 128 + 32 * j) >> 5) ^ q) << 6);
+    b_off[j] = lane_base + ((((wn * 128 + 32 * j) >> 5) ^ q) << 6);
+  }
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x16(0.f);
+
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j < nt) {
+      stage_op_w4(A, pa, lda, kbeg + j * TK2, lds0 + j * STAGEB2, w);
+      stage_op_w4(B, pb, ldb, kbeg + j * TK2, lds0 + j * STAGEB2 + OPB2, w);
+    }
+  }
+  // k-tile 0 landed (k-tile 1 may stay in flight)
+  if (nt > 1) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+
+  auto read_step = [&](const char LDS_AS* st, int ks, bf16x8 (&af)[4], bf16x8 (&bf)[4]) {
+    const char LDS_AS* sa = st;
+    const char LDS_AS* sb = st + OPB2;
+    const int ko = ks * 16 * ROWB;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) af[j] = tr_pair(sa + a_off[j] + ko, sa + a_off[j] + ko + 4 * ROWB);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = tr_pair(sb + b_off[j] + ko, sb + b_off[j] + ko + 4 * ROWB);
+  };
+
+  bf16x8 a0[4], b0[4], a1[4], b1[4];
+  read_step(smem, 0, a0, b0);
+  for (int t = 0; t < nt; ++t) {
+    const char LDS_AS* st = smem + (t & (NSTAGE2 - 1)) * STAGEB2;
+    if (t + 2 < nt) {  // DMA two k-tiles ahead into the stage k-tile t-2 used
+      const unsigned dst = lds0 + ((t + 2) & (NSTAGE2 - 1)) * STAGEB2;
+      stage_op_w4(A, pa, lda, kbeg + (long)(t + 2) * TK2, dst, w);
+      stage_op_w4(B, pb, ldb, kbeg + (long)(t + 2) * TK2, dst + OPB2, w);
+    }
+    // k-step 0 (fragments read before) while k-step 1's fragments are read
+    read_step(st, 1, a1, b1);
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma(a0[mb], b0[nb], acc[mb][nb]);
+    // k-step 1, first half
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma(a1[mb], b1[nb], acc[mb][nb]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nt) {
+      // k-tile t+1 landed (t+2 may stay in flight); publish, then read its k-step 0 under the
+      // second half of this k-step's MFMAs
+      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      read_step(smem + ((t + 1) & (NSTAGE2 - 1)) * STAGEB2, 0, a0, b0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mb = 2; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma(a1[mb], b1[nb], acc[mb][nb]);
+  }
+
+  const int c32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      // one 32x32 block at a time: the C loads of the beta path must not be hoisted for all 16
+      // blocks at once (256 extra VGPRs next to the 256 accumulators)
+      __builtin_amdgcn_sched_barrier(0);
+      const long n = n0 + wn * 128 + 32 * nb + c32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (SPLIT) {
+          slab[((long)split * M + m) * N + n] = acc[mb][nb][r];
+        } else {
+          float v = acc[mb][nb][r];
+          if (beta) v += bf2f(C[m * ldc + n]);
+          C[m * ldc + n] = f2bf(v);
+        }
+      }
+    }
+}
+
 // C[m][n] (+)= sum over splits of slab[s][m][n], 8 elements per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
                                                              long ldc, int M, int N, int splitk, int beta) {
@@ -519,7 +664,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // workspace of splitk*M*N floats.  Returns -1 for shapes the kernel does not tile.
 // flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop;
 //        bit1 = ping-pong v2 (k-tiles of 32, 4-stage ring, per-group DMA two k-tiles ahead);
-//        bit2 (with bit1) = DMA three k-tiles ahead
+//        bit2 (with bit1) = DMA three k-tiles ahead;
+//        bit3 = one wave per SIMD, 128 x 128 per wave (gemm_tn_w4_kernel, 256 threads)
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -543,7 +689,10 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
     if (splitk > 1) KERNEL<true, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
     else KERNEL<false, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
   } while (0)
-  if (pp2 && (flags & 4)) TH_TN_LAUNCH2(gemm_tn_pp2_kernel, 3);
+  if (flags & 8) {
+    if (splitk > 1) gemm_tn_w4_kernel<true><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta);
+    else gemm_tn_w4_kernel<false><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);
+  } else if (pp2 && (flags & 4)) TH_TN_LAUNCH2(gemm_tn_pp2_kernel, 3);
   else if (pp2) TH_TN_LAUNCH2(gemm_tn_pp2_kernel, 2);
   else if (pp) TH_TN_LAUNCH(gemm_tn_pp_kernel);
   else TH_TN_LAUNCH(gemm_tn_kernel);
