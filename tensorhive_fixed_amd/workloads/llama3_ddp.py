@@ -83,9 +83,9 @@ class Trainer:
         self.model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
         self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb,
                                     shard=self.zero >= 1 and info.world > 1)
-        if self.store.sharded:
-            self.model.param_gate = self.store.wait_params
         self.opt = FlatAdamW(self.store, lr=lr)
+        if self.store.sharded or self.opt.overlap:
+            self.model.param_gate = self.store.wait_params
         self.data = SyntheticTokens(cfg.vocab_size, micro_batch, seq_len, dev, info.rank)
         self.tokens_per_step = micro_batch * seq_len * grad_accum  # per rank
         self.last_loss: torch.Tensor | None = None
@@ -99,6 +99,8 @@ class Trainer:
                 self.store.begin_microbatch(accumulate=mb > 0, sync=mb == self.grad_accum - 1)
                 with _Range("forward"):
                     loss = self.model(tokens, targets, n_valid=n_valid * self.grad_accum)
+                if mb == 0:
+                    self.opt.wait_done()  # the previous step's (overlapped) update read these gradients
                 with _Range("backward"):
                     loss.backward()
                 loss_acc = loss.detach() if loss_acc is None else loss_acc + loss.detach()
@@ -116,6 +118,7 @@ class Trainer:
         """Everything a bit-exact resume needs: flat params, f32 master / moments, step, data RNG.
         With a sharded optimizer the moments are this rank's slices (see :meth:`save`)."""
         self.store.wait_all_params()
+        self.opt.wait_done()
         st = {"param_buf": self.store.param_buf, "step": torch.tensor(self.opt.step_count),
               "data_drawn": torch.tensor(self.data.drawn), "names": "\n".join(self.store.names),
               "zero_world": torch.tensor(self.info.world if self.store.sharded else 0)}
