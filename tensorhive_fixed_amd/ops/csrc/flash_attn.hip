@@ -549,7 +549,13 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     for (int s = 0; s < 8; ++s) sacc = mfma(lds_row(qs, c32, 2 * s + h), lds_row(ks, krow, 2 * s + h), sacc);
 #pragma unroll
     for (int s = 0; s < 8; ++s) pacc = mfma(lds_row(gs, c32, 2 * s + h), lds_row(vs, krow, 2 * s + h), pacc);
-    const bool need_mask = (causal && qbase < k0 + 31) || key >= S;
+    // Masking is branch-free inside the tile: a wave-uniform test decides whether this tile needs
+    // it at all, then every element is a select.  (Written as `if (need_mask && (key >= S || ...))`
+    // the short-circuit logic compiled to three exec-mask branches PER ELEMENT -- 45 saveexec
+    // blocks per iteration.)  Query row ro + 4h sees this key iff key - qbase - 4h <= ro.
+    const bool tile_mask = (causal && qbase < k0 + 31) || (k0 + 31 >= S);  // wave-uniform
+    const int kq = causal ? key - qbase - 4 * h : -0x40000000;
+    const bool koob = key >= S;
     // lse / delta of the accumulator rows (4h + (r&3) + 8(r>>2)): four 16-byte reads each
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -559,7 +565,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e, ro = e + 8 * g;
         float p = fast_exp2(sacc[r] * scale_log2 - lv[e]);
-        if (need_mask && (key >= S || (causal && key > qbase + ro + 4 * h))) p = 0.f;
+        if (tile_mask) p = (koob | (kq > ro)) ? 0.f : p;
         sacc[r] = p;
         pacc[r] = p * (pacc[r] - dv4[e]);
       }
