@@ -517,14 +517,19 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
   auto prefetch = [&](int h_i, int t_i) {
     const int hq = hk * G + h_i;
     const int qq0 = (qt0 + t_i) * B_BQ;
-    const bool ok = qq0 + srow < S;
-    qr = ok ? *reinterpret_cast<const ushort8*>(Q + b * bs + (long)hq * HD + (long)(qq0 + srow) * ld + (sch << 3)) : ushort8(0);
-    gr = ok ? *reinterpret_cast<const ushort8*>(dO + b * bso + (long)hq * HD + (long)(qq0 + srow) * ldo + (sch << 3)) : ushort8(0);
+    // rows past S are clamped to S-1 (finite data; their lse = +inf makes P and dS exactly 0), so
+    // the loads are unconditional: no exec-mask branch around them
+    const int row = min(qq0 + srow, S - 1);
+    qr = *reinterpret_cast<const ushort8*>(Q + b * bs + (long)hq * HD + (long)row * ld + (sch << 3));
+    gr = *reinterpret_cast<const ushort8*>(dO + b * bso + (long)hq * HD + (long)row * ldo + (sch << 3));
     if (tid < B_BQ) {
       const int qq = qq0 + tid;
       const long st = ((long)b * Hq + hq) * S;
-      lr = qq < S ? LSE[st + qq] : INFINITY;  // scaled by log2(e) when stored: no use right after the load
-      dr = qq < S ? Dl[st + qq] : 0.f;
+      const int qc = min(qq, S - 1);
+      lr = LSE[st + qc];  // scaled by log2(e) when stored: no use right after the load
+      dr = Dl[st + qc];
+      lr = qq < S ? lr : INFINITY;
+      dr = qq < S ? dr : 0.f;
     }
   };
   if (total > 0) prefetch(0, 0);
