@@ -354,6 +354,9 @@ __global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict_
 }
 
 // ------------------------------------------------------------------------------- dQ kernel
+#ifndef TH_DQ_AHEAD
+#define TH_DQ_AHEAD 1  // 0: reads issued right before their MFMA (compiler order)
+#endif
 template <bool KVMAJOR>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
@@ -410,24 +413,70 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {  // 32-key halves: keeps only one S^T / dP^T pair live
       f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+#if TH_DQ_AHEAD
+      {  // K/V row operands read two k-steps ahead of the MFMAs that use them (2 gaps of latency cover)
+        bf16x8 ka[2], va[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          ka[s] = lds_row(ks, 32 * kb + c32, 2 * s + h);
+          va[s] = lds_row(vs, 32 * kb + c32, 2 * s + h);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          bf16x8 kn = ka[s & 1], vn = va[s & 1];
+          if (s + 2 < 8) {
+            kn = lds_row(ks, 32 * kb + c32, 2 * s + 4 + h);
+            vn = lds_row(vs, 32 * kb + c32, 2 * s + 4 + h);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          sacc = mfma(ka[s & 1], qf[s], sacc);
+          pacc = mfma(va[s & 1], gf[s], pacc);
+          __builtin_amdgcn_sched_barrier(0);
+          ka[s & 1] = kn;
+          va[s & 1] = vn;
+        }
+      }
+#else
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         sacc = mfma(lds_row(ks, 32 * kb + c32, 2 * s + h), qf[s], sacc);
         pacc = mfma(lds_row(vs, 32 * kb + c32, 2 * s + h), gf[s], pacc);
       }
-      const int kmax = (causal ? min(q, S - 1) : S - 1) - kbase - 32 * kb - 4 * h;  // tile-relative
+#endif
+      // tile-relative last visible key of this lane's query (INT_MAX: the tile needs no mask)
+      const int kmax = need_mask ? (causal ? min(q, S - 1) : S - 1) - kbase - 32 * kb - 4 * h : 0x7fffffff;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float p = fast_exp2(sacc[r] * scale_log2 - lse2);
-        if (need_mask) p = ((r & 3) + 8 * (r >> 2) <= kmax) ? p : 0.f;
+        p = ((r & 3) + 8 * (r >> 2) <= kmax) ? p : 0.f;
         sacc[r] = p * (pacc[r] - dlt);  // dS^T
       }
       const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
+#if TH_DQ_AHEAD
+      {  // K^T operands one d-step ahead
+        bf16x8 t0 = lds_tr(ks, 32 * kb, 0, lane), t1 = lds_tr(ks, 32 * kb + 16, 0, lane);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          bf16x8 n0 = t0, n1 = t1;
+          if (d < 3) {
+            n0 = lds_tr(ks, 32 * kb, 32 * d + 32, lane);
+            n1 = lds_tr(ks, 32 * kb + 16, 32 * d + 32, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          dq[d] = mfma(t0, s0, dq[d]);
+          dq[d] = mfma(t1, s1, dq[d]);
+          __builtin_amdgcn_sched_barrier(0);
+          t0 = n0;
+          t1 = n1;
+        }
+      }
+#else
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         dq[d] = mfma(lds_tr(ks, 32 * kb, 32 * d, lane), s0, dq[d]);
         dq[d] = mfma(lds_tr(ks, 32 * kb + 16, 32 * d, lane), s1, dq[d]);
       }
+#endif
     }
   }
   if (q < S) {
@@ -560,7 +609,9 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
     // blocks per iteration.)  Query row ro + 4h sees this key iff key - qbase - 4h <= ro.
     const bool tile_mask = (causal && qbase < k0 + 31) || (k0 + 31 >= S);  // wave-uniform
     const int kq = causal ? key - qbase - 4 * h : -0x40000000;
-    const bool koob = key >= S;
+    // one per-lane threshold: the element (row ro) is zeroed iff mthr > ro (no per-element SALU
+    // mask algebra: a v_cmp + v_cndmask each)
+    const int mthr = tile_mask ? (key >= S ? 0x7fffffff : kq) : -0x7fffffff;
     // lse / delta of the accumulator rows (4h + (r&3) + 8(r>>2)): four 16-byte reads each
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -570,7 +621,7 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e, ro = e + 8 * g;
         float p = fast_exp2(sacc[r] * scale_log2 - lv[e]);
-        if (tile_mask) p = (koob | (kq > ro)) ? 0.f : p;
+        p = mthr > ro ? 0.f : p;
         sacc[r] = p;
         pacc[r] = p * (pacc[r] - dv4[e]);
       }
