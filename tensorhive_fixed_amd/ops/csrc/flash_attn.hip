@@ -12,8 +12,10 @@
 //                        except one lane^32 exchange, and the O^T rescale is per-lane).
 //   dQ       (query-centric, same skeleton):  S^T, dP^T = V dO^T, dS^T = P^T (dP^T - delta),
 //            dQ^T += K^T dS^T  (K^T via transposed LDS reads).  No atomics: deterministic.
-//   dK/dV    (key-centric, 4 waves x 32 keys, loops over the GQA group's query heads):
+//   dK/dV    (key-centric, loops over the GQA group's query heads):
 //            S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS.
+//            Default: the paired kernel (dK waves and dV waves of 128 keys share the Q/dO tile,
+//            K/V in registers); flags bit3: the fused kernel (8 waves x 32 keys, K/V in LDS).
 //
 // Every LDS tile uses ONE image that serves both 16-byte row reads and transposed reads
 // conflict-free (8-row x 32-column subtiles, see img_off).
@@ -657,6 +659,184 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
       }
   }
 }
+// ------------------------------------------------------------ paired key-centric dK | dV kernel
+// The fused dK/dV kernel above needs 128 accumulator VGPRs (dK and dV) and so cannot keep its
+// K/V operands in registers: every S / dP MFMA reads BOTH operands from LDS, and the K/V block
+// costs 128 KB of LDS.  Here a workgroup of 8 waves covers 128 keys with two ROLES:
+//   waves 0-3, dK role: S = Q K^T, dP = dO V^T, dS = P (dP - delta), dK^T += Q^T dS  (3 units)
+//   waves 4-7, dV role: S = Q K^T, P,                                 dV^T += dO^T P (2 units)
+// S is computed twice (5 GEMM units per (q, k) pair instead of 4), but each wave holds only 64
+// accumulator VGPRs, so K (and V) fragments stay in registers for the whole kernel and each
+// S / dP MFMA reads one operand from LDS (like the dQ kernel).  The two roles share one staged
+// 64-query Q/dO tile (the dK waves stage Q + lse + delta, the dV waves dO): the Q/dO stream is
+// read once per 128 keys.  B4 S4096 32/8 heads: backward 2.78 -> 2.53 ms (profiles/r01_flash_v3).
+// (One role per workgroup, streaming the tile twice, measured no faster than the fused kernel.)
+constexpr int C_BK = 128, C_BQ = 64;
+
+template <bool DK>
+__device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
+                                        const float* __restrict__ LSE, const float* __restrict__ Dl,
+                                        const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
+                                        char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
+                                        long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  char* qs = smem;
+  char* gs = smem + C_BQ * 256;
+  float* ls = reinterpret_cast<float*>(smem + 2 * C_BQ * 256);
+  float* ds = ls + C_BQ;
+  // role-local thread id: waves 0-3 are the dK role, 4-7 the dV role of the same 128 keys
+  const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  const int k0 = kblk0 + 32 * w;
+  const int key = k0 + c32;
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(Kb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
+    if (DK) vf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(Vb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
+  }
+  f32x16 acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
+
+  const int nqt = (S + C_BQ - 1) / C_BQ;
+  const int qt0 = causal ? kblk0 / C_BQ : 0;
+  const int per_head = nqt - qt0;
+  const int total = G * per_head;
+  ushort8 xr[4];  // the dK role stages the Q tile (+ lse, delta), the dV role the dO tile
+  float lr = 0.f, dr = 0.f;
+  int pf_h = 0, pf_t = 0, cur_t = 0;
+  auto prefetch = [&](int h_i, int t_i) {
+    const int hq = hk * G + h_i;
+    const int qq0 = (qt0 + t_i) * C_BQ;
+    if (DK)
+      stage_load<4>(xr, Q + b * bs + (long)hq * HD, ld, qq0, S, tid);
+    else
+      stage_load<4>(xr, dO + b * bso + (long)hq * HD, ldo, qq0, S, tid);
+    if (DK && tid < C_BQ) {
+      const int qq = qq0 + tid;
+      const long st = ((long)b * Hq + hq) * S;
+      const int qc = min(qq, S - 1);
+      lr = LSE[st + qc];  // LOG2E-scaled when stored
+      dr = Dl[st + qc];
+      lr = qq < S ? lr : INFINITY;  // rows past S: P = 0 exactly
+      dr = qq < S ? dr : 0.f;
+    }
+  };
+  if (total > 0) prefetch(0, 0);
+  for (int it = 0; it < total; ++it) {
+    __syncthreads();
+    stage_store<4>(DK ? qs : gs, xr, tid);
+    if (DK && tid < C_BQ) {
+      ls[tid] = lr * LOG2E;
+      ds[tid] = dr;
+    }
+    __syncthreads();
+    const int qbase = (qt0 + cur_t) * C_BQ;
+    if (++cur_t == per_head) cur_t = 0;
+    if (++pf_t == per_head) { pf_t = 0; ++pf_h; }
+    if (it + 1 < total) prefetch(pf_h, pf_t);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {  // 32-query halves
+      const int q0 = qbase + 32 * kb;
+      if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
+      f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+      {  // Q / dO row operands read two k-steps ahead of their MFMAs
+        bf16x8 qa[2], ga[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          qa[s] = lds_row(qs, 32 * kb + c32, 2 * s + h);
+          if (DK) ga[s] = lds_row(gs, 32 * kb + c32, 2 * s + h);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          bf16x8 qn = qa[s & 1], gn = ga[s & 1];
+          if (s + 2 < 8) {
+            qn = lds_row(qs, 32 * kb + c32, 2 * s + 4 + h);
+            if (DK) gn = lds_row(gs, 32 * kb + c32, 2 * s + 4 + h);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          sacc = mfma(qa[s & 1], kf[s], sacc);
+          if (DK) pacc = mfma(ga[s & 1], vf[s], pacc);
+          __builtin_amdgcn_sched_barrier(0);
+          qa[s & 1] = qn;
+          if (DK) ga[s & 1] = gn;
+        }
+      }
+      // element r of the lane is query row q0 + 4h + ro (ro = (r&3) + 8(r>>2)), key column `key`:
+      // masked iff key > query, i.e. mthr > ro (one v_cmp + v_cndmask per element)
+      const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform
+      const int mthr = tile_mask ? key - q0 - 4 * h : -0x7fffffff;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
+        float4v dv4;
+        if (DK) dv4 = *reinterpret_cast<const float4v*>(ds + 32 * kb + 4 * h + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e, ro = e + 8 * g;
+          float p = fast_exp2(sacc[r] * scale_log2 - lv[e]);
+          p = mthr > ro ? 0.f : p;
+          sacc[r] = DK ? p * (pacc[r] - dv4[e]) : p;
+        }
+      }
+      const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
+      const char* op = DK ? qs : gs;  // dK^T += Q^T dS ; dV^T += dO^T P
+      bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        bf16x8 n0 = t0, n1 = t1;
+        if (d < 3) {
+          n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
+          n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc[d] = mfma(t0, s0, acc[d]);
+        acc[d] = mfma(t1, s1, acc[d]);
+        __builtin_amdgcn_sched_barrier(0);
+        t0 = n0;
+        t1 = n1;
+      }
+    }
+  }
+  if (key < S) {
+    ushort* orow = out + b * bs + (long)key * ld + (long)hk * HD;
+    const float f = DK ? scale : 1.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4v o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[d][4 * g + e] * f);
+        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = o;
+      }
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * C_BQ * 256 + 2 * C_BQ * 4];
+  const int nkb = (S + C_BK - 1) / C_BK;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  // (batch, kv head)-major: the key blocks of one group run together on an XCD and share its
+  // Q/dO stream in L2 (key-block-major across groups measured 1.6x slower)
+  const int grp = L / nkb, kb_i = L % nkb;
+  const int b = grp / Hkv, hk = grp % Hkv;
+  const int kblk = causal ? kb_i : nkb - 1 - kb_i;
+  const int G = Hq / Hkv;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+  // wave-uniform role split; both roles pass the same barriers (same tile sequence)
+  if (threadIdx.x >= 256)
+    kc_body<false>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+                   scale_log2, causal);
+  else
+    kc_body<true>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+                  scale_log2, causal);
+}
+
 constexpr int B_LDS = 2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4;
 }  // namespace
 
@@ -717,6 +897,14 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
     fa_bwd_dq_kernel<true><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                         (const ushort*)dout, lse, delta, (ushort*)dq, B, S,
                                                         Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+  // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernel)
+  if (!(flags & 8)) {
+    const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;
+    fa_bwd_kc_kernel<<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                   (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv, B,
+                                                   S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+    TH_CHECK_LAUNCH();
+  }
   const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;
   static bool attr_set = false;
   if (!attr_set) {

@@ -13,8 +13,9 @@ def _ref(qkv, B, S, Hq, Hkv, D, causal=True):
     return attention_reference(q, k, v, causal).reshape(B * S, Hq * D)
 
 
+@pytest.mark.parametrize("bwd_flags", [0, 8], ids=["split_kc", "fused_dkv"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 128, 4, 1), (2, 200, 8, 2), (1, 1024, 32, 8), (1, 64, 2, 2)])
-def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv):
+def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
     torch.manual_seed(0)
     D = 128
@@ -35,7 +36,7 @@ def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv):
     assert (lse - lse_ref).abs().max().item() < 1e-2
     do = torch.randn_like(o)
     ref.backward(do.float())
-    dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)
+    dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D, flags=bwd_flags)
     g = x.grad
     for name, a, b in (("dq", dqkv[:, : Hq * D], g[:, : Hq * D]),
                        ("dk", dqkv[:, Hq * D:(Hq + Hkv) * D], g[:, Hq * D:(Hq + Hkv) * D]),
@@ -59,3 +60,21 @@ def test_qkv_attention_with_rope_matches_sdpa_path():
     ob.backward(g)
     rel = ((a.grad.float() - b.grad.float()).norm() / b.grad.float().norm()).item()
     assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("bwd_flags", [0, 8], ids=["split_kc", "fused_dkv"])
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 200, 8, 2), (1, 384, 4, 4)])
+def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
+    from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
+    torch.manual_seed(1)
+    D = 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D, causal=False)
+    x = qkv.float().requires_grad_(True)
+    ref = _ref(x, B, S, Hq, Hkv, D, causal=False)
+    assert (o.float() - ref).abs().max().item() < 2e-2
+    do = torch.randn_like(o)
+    ref.backward(do.float())
+    dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D, causal=False, flags=bwd_flags)
+    rel = ((dqkv.float() - x.grad).norm() / x.grad.norm()).item()
+    assert rel < 2e-2, f"dqkv rel err {rel}"
