@@ -662,16 +662,21 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
 // ------------------------------------------------------------ paired key-centric dK | dV kernel
 // The fused dK/dV kernel above needs 128 accumulator VGPRs (dK and dV) and so cannot keep its
 // K/V operands in registers: every S / dP MFMA reads BOTH operands from LDS, and the K/V block
-// costs 128 KB of LDS.  Here a workgroup of 8 waves covers 128 keys with two ROLES:
-//   waves 0-3, dK role: S = Q K^T, dP = dO V^T, dS = P (dP - delta), dK^T += Q^T dS  (3 units)
-//   waves 4-7, dV role: S = Q K^T, P,                                 dV^T += dO^T P (2 units)
-// S is computed twice (5 GEMM units per (q, k) pair instead of 4), but each wave holds only 64
-// accumulator VGPRs, so K (and V) fragments stay in registers for the whole kernel and each
-// S / dP MFMA reads one operand from LDS (like the dQ kernel).  The two roles share one staged
-// 64-query Q/dO tile (the dK waves stage Q + lse + delta, the dV waves dO): the Q/dO stream is
-// read once per 128 keys.  B4 S4096 32/8 heads: backward 2.78 -> 2.53 ms (profiles/r01_flash_v3).
-// (One role per workgroup, streaming the tile twice, measured no faster than the fused kernel.)
-constexpr int C_BK = 128, C_BQ = 64;
+// costs 128 KB of LDS.  Here a workgroup of 8 waves covers 128 keys, and each 32-key slice is
+// owned by a PAIR of waves with one accumulator each:
+//   dV wave (4-7):  phase 1  S = Q K^T -> P (registers + LDS exchange)   phase 2  dV^T += dO^T P
+//   dK wave (0-3):  phase 1  dP = dO V^T                                 phase 2  dS = P (dP - delta),
+//                                                                                 dK^T += Q^T dS
+// Both roles run 16 + 16 MFMAs per 64-query tile (balanced, no GEMM recomputed), hold only 64
+// accumulator VGPRs, keep their K (dV wave) or V (dK wave) fragments in registers for the whole
+// kernel, and read one MFMA operand per instruction from LDS (like the dQ kernel).  P crosses
+// from the dV wave to its partner as f32 through an 8 KB lane-linear LDS slot (conflict-free
+// ds_write/read_b128), one barrier between the phases.  The pair shares one staged Q/dO tile
+// (the dK waves stage Q + lse + delta, the dV waves dO).
+// B4 S4096 32/8 heads: backward 2.64 -> 2.29 ms against the fused kernel (profiles/r01_flash_v3).
+// (Measured on the way: one role per workgroup streaming the tile twice = no faster than the
+// fused kernel; paired roles that each recompute S = -9 %; LDS double-buffering = no change.)
+constexpr int C_BK = 128, C_BQ = 64, KC_TILE = 2 * C_BQ * 256 + 2 * C_BQ * 4;
 
 template <bool DK>
 __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
@@ -685,14 +690,16 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
   float* ds = ls + C_BQ;
   // role-local thread id: waves 0-3 are the dK role, 4-7 the dV role of the same 128 keys
   const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  // P exchange of wave pair w: [half][4 x float4][lane], 8 KB
+  float4v* pbuf = reinterpret_cast<float4v*>(smem + KC_TILE + w * 8192);
   const int k0 = kblk0 + 32 * w;
   const int key = k0 + c32;
-  bf16x8 kf[8], vf[8];
+  // dK role: V fragments (dP = dO V^T); dV role: K fragments (S = Q K^T)
+  const ushort* fb = DK ? Vb : Kb;
+  bf16x8 kf[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(Kb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
-    if (DK) vf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(Vb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
-  }
+  for (int s = 0; s < 8; ++s)
+    kf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
   f32x16 acc[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
@@ -734,51 +741,61 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
     if (++cur_t == per_head) cur_t = 0;
     if (++pf_t == per_head) { pf_t = 0; ++pf_h; }
     if (it + 1 < total) prefetch(pf_h, pf_t);
+    // phase 1 (both 32-query halves): dK role dP = dO V^T, dV role S = Q K^T -> P (to LDS)
+    f32x16 c[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {  // 32-query halves
+    for (int kb = 0; kb < 2; ++kb) {
       const int q0 = qbase + 32 * kb;
+      c[kb] = f32x16(0.f);
       if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
-      f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
-      {  // Q / dO row operands read two k-steps ahead of their MFMAs
-        bf16x8 qa[2], ga[2];
+      const char* img = DK ? gs : qs;
+      bf16x8 xa[2];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          qa[s] = lds_row(qs, 32 * kb + c32, 2 * s + h);
-          if (DK) ga[s] = lds_row(gs, 32 * kb + c32, 2 * s + h);
-        }
+      for (int s = 0; s < 2; ++s) xa[s] = lds_row(img, 32 * kb + c32, 2 * s + h);
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          bf16x8 qn = qa[s & 1], gn = ga[s & 1];
-          if (s + 2 < 8) {
-            qn = lds_row(qs, 32 * kb + c32, 2 * s + 4 + h);
-            if (DK) gn = lds_row(gs, 32 * kb + c32, 2 * s + 4 + h);
+      for (int s = 0; s < 8; ++s) {  // row operands read two k-steps ahead
+        bf16x8 xn = xa[s & 1];
+        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
+        __builtin_amdgcn_sched_barrier(0);
+        c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
+        __builtin_amdgcn_sched_barrier(0);
+        xa[s & 1] = xn;
+      }
+      if (!DK) {
+        // element r of the lane is query row q0 + 4h + ro (ro = (r&3) + 8(r>>2)), key column
+        // `key`: masked iff key > query, i.e. mthr > ro
+        const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform
+        const int mthr = tile_mask ? key - q0 - 4 * h : -0x7fffffff;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
+          float4v pv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float p = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
+            pv[e] = mthr > e + 8 * g ? 0.f : p;
+            c[kb][4 * g + e] = pv[e];
           }
-          __builtin_amdgcn_sched_barrier(0);
-          sacc = mfma(qa[s & 1], kf[s], sacc);
-          if (DK) pacc = mfma(ga[s & 1], vf[s], pacc);
-          __builtin_amdgcn_sched_barrier(0);
-          qa[s & 1] = qn;
-          if (DK) ga[s & 1] = gn;
+          pbuf[(kb * 4 + g) * 64 + lane] = pv;
         }
       }
-      // element r of the lane is query row q0 + 4h + ro (ro = (r&3) + 8(r>>2)), key column `key`:
-      // masked iff key > query, i.e. mthr > ro (one v_cmp + v_cndmask per element)
-      const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform
-      const int mthr = tile_mask ? key - q0 - 4 * h : -0x7fffffff;
+    }
+    __syncthreads();  // P of every pair visible
+    // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
-        float4v dv4;
-        if (DK) dv4 = *reinterpret_cast<const float4v*>(ds + 32 * kb + 4 * h + 8 * g);
+    for (int kb = 0; kb < 2; ++kb) {
+      const int q0 = qbase + 32 * kb;
+      if (causal && q0 + 31 < k0) continue;
+      if (DK) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e, ro = e + 8 * g;
-          float p = fast_exp2(sacc[r] * scale_log2 - lv[e]);
-          p = mthr > ro ? 0.f : p;
-          sacc[r] = DK ? p * (pacc[r] - dv4[e]) : p;
+        for (int g = 0; g < 4; ++g) {
+          const float4v pv = pbuf[(kb * 4 + g) * 64 + lane];
+          const float4v dv4 = *reinterpret_cast<const float4v*>(ds + 32 * kb + 4 * h + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = pv[e] * (c[kb][4 * g + e] - dv4[e]);
         }
       }
-      const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
+      const bf16x8 s0 = pack8(c[kb], 0), s1 = pack8(c[kb], 8);
       const char* op = DK ? qs : gs;  // dK^T += Q^T dS ; dV^T += dO^T P
       bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
 #pragma unroll
@@ -817,7 +834,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
     long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * C_BQ * 256 + 2 * C_BQ * 4];
+  __shared__ __attribute__((aligned(16))) char smem[KC_TILE + 4 * 8192];  // tile | P exchange
   const int nkb = (S + C_BK - 1) / C_BK;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   // (batch, kv head)-major: the key blocks of one group run together on an XCD and share its
