@@ -88,6 +88,11 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
     return o, lse
 
 
+# launch flags of the backward (th_flash_attn_bwd): bit0 q-major dQ order, bit1/bit2 fused dK/dV
+# order / priority, bit3 the fused dK/dV kernel instead of the paired one -- A/B aid
+_BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", "0"))
+
+
 def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, B: int,
               S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True, flags: int = 0) -> torch.Tensor:
     """HIP flash attention backward -> dqkv in the packed layout."""
@@ -134,7 +139,7 @@ class _QKVAttention(torch.autograd.Function):
         B, S, Hq, Hkv, Dh, theta = ctx.dims
         if ctx.backend == "hip" and do.is_cuda:
             qkv, o, lse = ctx.saved_tensors
-            dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh)
+            dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh, flags=_BWD_FLAGS)
         else:
             (qkv,) = ctx.saved_tensors
             with torch.enable_grad():
