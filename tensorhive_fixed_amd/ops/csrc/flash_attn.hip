@@ -140,9 +140,40 @@ __device__ __forceinline__ void q_block_map(int L, int nqb, int B, int Hq, int H
   }
 }
 
+// ------------------------------------------------------------------ LDS-DMA tile staging
+// global_load_lds_dwordx4 (inline asm with a scalar base: the builtin makes the compiler drain
+// vmcnt before every later ds_read) writes 16 B per lane lane-linearly at M0.  For a 64-row x
+// 128-col bf16 tile in the img_off image (16 KB), wave w issues 4 x 1 KB: lane l of instruction u
+// fills image byte o = 4096w + 1024u + 16l, so it loads the (row, chunk) that img_off maps to o.
+// No staging VGPRs, no ds_write, one barrier per tile (double-buffered images).
+__device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
+}
+// (row | chunk << 8) of image byte o (inverse of img_off)
+__device__ __forceinline__ unsigned img_rc(unsigned o) {
+  const unsigned row = ((o >> 11) << 3) | ((o >> 6) & 7);
+  const unsigned ch = (((o >> 9) & 3) << 2) | (((o >> 4) & 3) ^ ((row >> 2) & 3));
+  return row | (ch << 8);
+}
+__device__ __forceinline__ void wait_dma_barrier() { asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); }
+// K and V rows 64jt .. +63 (clamped to S-1) into image pair jt & 1 at lds0 (pairs of 2 x 16 KB);
+// rc[u] = img_rc(4096w + 1024u + 16 lane), wu = wave index (scalar)
+__device__ __forceinline__ void dma_kv_tile(const ushort* Kb, const ushort* Vb, long ld, int S, int jt, unsigned lds0,
+                                            int wu, const unsigned (&rc)[4]) {
+  const unsigned img = lds0 + (jt & 1) * (2 * 64 * 256) + wu * 4096;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = min(jt * 64 + (int)(rc[u] & 255), S - 1);
+    const unsigned voff = (unsigned)(row * ld + (rc[u] >> 8) * 8) * 2u;
+    glds16(Kb, voff, img + u * 1024);
+    glds16(Vb, voff, img + 64 * 256 + u * 1024);
+  }
+}
+
 // --------------------------------------------------------------------------------- forward
 #ifndef TH_FA_FWD_DEFAULT
-#define TH_FA_FWD_DEFAULT 11  // PRESCALE + DEFER + KVMAJOR: 747 vs 447 TFLOP/s for 0 (B4 S4096, profiles/r01_flash)
+#define TH_FA_FWD_DEFAULT 15  // PRESCALE + DEFER + DMA-staged DBUF + KVMAJOR: 937 vs 829 TFLOP/s for 11 (B4 S4096, profiles/r01_flash_v3)
 #endif
 constexpr int F_BM = 128, F_BN = 64;
 constexpr float F_DEFER_THR = 8.f;  // log2 units: P may reach 2^8 before O/l are rescaled
@@ -165,7 +196,8 @@ __device__ __forceinline__ float half_swap_sum(float x) {
 // Variant knobs (flags of th_flash_attn_fwd):
 //   PRESCALE  fold softmax_scale*log2(e) into Q once (no per-score multiply)
 //   DEFER     skip the O/l rescale while the running max grows by <= F_DEFER_THR (wave-uniform)
-//   DBUF      double-buffered K/V LDS tiles: ONE barrier per key tile instead of two
+//   DBUF      LDS-DMA staging into double-buffered K/V images: no staging VGPRs / ds_writes, ONE
+//             barrier per key tile instead of two
 template <bool PRESCALE, bool DEFER, bool DBUF, bool KVMAJOR>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
@@ -200,12 +232,17 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
   const int ntiles = (kv_end + F_BN - 1) / F_BN;
   ushort8 kr[4], vr[4];
-  stage_load<4>(kr, Kb, ld, 0, S, tid);
-  stage_load<4>(vr, Vb, ld, 0, S, tid);
-  if (DBUF) {
-    stage_store<4>(smem, kr, tid);
-    stage_store<4>(smem + F_BN * 256, vr, tid);
-    __syncthreads();
+  unsigned rc[4];
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  if (DBUF) {  // LDS-DMA staging (see dma_kv_tile); Q loads retired by a wait the compiler sees
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rc[u] = img_rc(w * 4096 + u * 1024 + lane * 16);
+    dma_kv_tile(Kb, Vb, ld, S, 0, lds0, wu, rc);
+  } else {
+    stage_load<4>(kr, Kb, ld, 0, S, tid);
+    stage_load<4>(vr, Vb, ld, 0, S, tid);
   }
 
   f32x16 o[4];
@@ -216,15 +253,18 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   for (int j = 0; j < ntiles; ++j) {
     char* ks = smem + (DBUF ? (j & 1) : 0) * (2 * F_BN * 256);
     char* vs = ks + F_BN * 256;
-    if (!DBUF) {
+    if (DBUF) {
+      wait_dma_barrier();  // tile j landed (every wave's DMA); everyone is past tile j-1
+      if (j + 1 < ntiles) dma_kv_tile(Kb, Vb, ld, S, j + 1, lds0, wu, rc);
+    } else {
       __syncthreads();
       stage_store<4>(ks, kr, tid);
       stage_store<4>(vs, vr, tid);
       __syncthreads();
-    }
-    if (j + 1 < ntiles) {
-      stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
-      stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
+      if (j + 1 < ntiles) {
+        stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
+        stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
+      }
     }
     const int kbase = j * F_BN;
     if (!(causal && kbase > q0 + 31)) {  // wave-uniform: tile entirely above the diagonal is skipped
@@ -324,12 +364,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         FA_PRIO(0);
       }
     }
-    if (DBUF && j + 1 < ntiles) {
-      char* nk = smem + ((j + 1) & 1) * (2 * F_BN * 256);
-      stage_store<4>(nk, kr, tid);
-      stage_store<4>(nk + F_BN * 256, vr, tid);
-      __syncthreads();
-    }
   }
 
   if (q < S) {
@@ -370,19 +404,19 @@ __global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict_
   if ((threadIdx.x & 15) == 0) delta[((long)b * Hq + hq) * S + q] = s;
 }
 
+
 // ------------------------------------------------------------------------------- dQ kernel
 #ifndef TH_DQ_AHEAD
 #define TH_DQ_AHEAD 1  // 0: reads issued right before their MFMA (compiler order)
 #endif
-template <bool KVMAJOR>
+template <bool KVMAJOR, bool DMA>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dQ, int B, int S, int Hq, int Hkv, long ld, long bs, long ldo, long bso,
     float scale, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * F_BN * 256];
-  char* ks = smem;
-  char* vs = smem + F_BN * 256;
+  // DMA: two K|V image pairs (64 KB), else one pair staged through registers
+  __shared__ __attribute__((aligned(1024))) char smem_dq[(DMA ? 2 : 1) * 2 * F_BN * 256];
   const int nqb = (S + F_BM - 1) / F_BM;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   int b, hq, qb;
@@ -409,20 +443,41 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
   const int ntiles = (kv_end + F_BN - 1) / F_BN;
   ushort8 kr[4], vr[4];
-  stage_load<4>(kr, Kb, ld, 0, S, tid);
-  stage_load<4>(vr, Vb, ld, 0, S, tid);
+  unsigned rc[4];
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem_dq;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto dma_tile = [&](int jt) { dma_kv_tile(Kb, Vb, ld, S, jt, lds0, wu, rc); };
+  if (DMA) {
+    // retire the Q / dO / LSE / delta loads HERE with a real s_waitcnt (vmcnt(0)) the compiler's
+    // wait insertion sees: otherwise it places the waits for them at their first use inside the
+    // loop, where each iteration would also wait for the tile DMA it has just issued
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rc[u] = img_rc(w * 4096 + u * 1024 + lane * 16);
+    dma_tile(0);
+  } else {
+    stage_load<4>(kr, Kb, ld, 0, S, tid);
+    stage_load<4>(vr, Vb, ld, 0, S, tid);
+  }
   f32x16 dq[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) dq[d] = f32x16(0.f);
 
   for (int j = 0; j < ntiles; ++j) {
-    __syncthreads();
-    stage_store<4>(ks, kr, tid);
-    stage_store<4>(vs, vr, tid);
-    __syncthreads();
-    if (j + 1 < ntiles) {
-      stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
-      stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
+    char* ks = smem_dq + (DMA ? (j & 1) * (2 * F_BN * 256) : 0);
+    char* vs = ks + F_BN * 256;
+    if (DMA) {
+      wait_dma_barrier();  // tile j landed (every wave's DMA); everyone is past tile j-1
+      if (j + 1 < ntiles) dma_tile(j + 1);
+    } else {
+      __syncthreads();
+      stage_store<4>(ks, kr, tid);
+      stage_store<4>(vs, vr, tid);
+      __syncthreads();
+      if (j + 1 < ntiles) {
+        stage_load<4>(kr, Kb, ld, (j + 1) * F_BN, S, tid);
+        stage_load<4>(vr, Vb, ld, (j + 1) * F_BN, S, tid);
+      }
     }
     const int kbase = j * F_BN;
     if (causal && kbase > q0 + 31) continue;
@@ -885,7 +940,8 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   const long nblk = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags: 0 = default variant; 16 + v = explicit v (bit0 PRESCALE, bit1 DEFER, bit2 DBUF,
   // bit3 KVMAJOR block order)
-  const int var = flags >= 16 ? (flags & 15) : TH_FA_FWD_DEFAULT;
+  int var = flags >= 16 ? (flags & 15) : TH_FA_FWD_DEFAULT;
+  if ((long)S * ld * 2 >= (1L << 31)) var &= ~4;  // DMA staging uses 32-bit row offsets
 #define TH_FWD(P, Dd, Db, Km)                                                                      \
   fa_fwd_kernel<P, Dd, Db, Km><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,  \
                                                              (const ushort*)v, (ushort*)o, lse, B,  \
@@ -903,7 +959,7 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
     case 8: TH_FWD(false, false, false, true); break;
     case 11: TH_FWD(true, true, false, true); break;
     case 15: TH_FWD(true, true, true, true); break;
-    default: TH_FWD(true, true, false, true); break;
+    default: TH_FWD(true, true, true, true); break;
   }
 #undef TH_FWD
   TH_CHECK_LAUNCH();
@@ -920,15 +976,19 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   fa_delta_kernel<<<(unsigned)((rows + 15) / 16), 256, 0, s>>>((const ushort*)o, (const ushort*)dout,
                                                                delta, B, S, Hq, ldo, bso);
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
-  // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map)
-  if (flags & 1)
-    fa_bwd_dq_kernel<false><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                         (const ushort*)dout, lse, delta, (ushort*)dq, B, S,
-                                                         Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
-  else
-    fa_bwd_dq_kernel<true><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                        (const ushort*)dout, lse, delta, (ushort*)dq, B, S,
-                                                        Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+  // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
+  // bit5: register-staged K/V tiles instead of LDS-DMA (also used when 32-bit offsets overflow)
+  const bool dq_dma = !(flags & 32) && (long)S * ld * 2 < (1L << 31);
+#define TH_DQ_LAUNCH(KVM, DMA_)                                                                              \
+  fa_bwd_dq_kernel<KVM, DMA_><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, \
+                                                           (const ushort*)dout, lse, delta, (ushort*)dq, B, S, Hq, \
+                                                           Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal)
+  if (flags & 1) {
+    if (dq_dma) TH_DQ_LAUNCH(false, true); else TH_DQ_LAUNCH(false, false);
+  } else {
+    if (dq_dma) TH_DQ_LAUNCH(true, true); else TH_DQ_LAUNCH(true, false);
+  }
+#undef TH_DQ_LAUNCH
   // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernel)
   if (!(flags & 8)) {
     const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;

@@ -13,7 +13,7 @@ def _ref(qkv, B, S, Hq, Hkv, D, causal=True):
     return attention_reference(q, k, v, causal).reshape(B * S, Hq * D)
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8], ids=["paired_kc", "fused_dkv"])
+@pytest.mark.parametrize("bwd_flags", [0, 8, 32], ids=["paired_kc", "fused_dkv", "dq_regstage"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 128, 4, 1), (2, 200, 8, 2), (1, 1024, 32, 8), (1, 64, 2, 2)])
 def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -62,7 +62,7 @@ def test_qkv_attention_with_rope_matches_sdpa_path():
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8], ids=["paired_kc", "fused_dkv"])
+@pytest.mark.parametrize("bwd_flags", [0, 8, 32], ids=["paired_kc", "fused_dkv", "dq_regstage"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 200, 8, 2), (1, 384, 4, 4)])
 def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -78,3 +78,14 @@ def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D, causal=False, flags=bwd_flags)
     rel = ((dqkv.float() - x.grad).norm() / x.grad.norm()).item()
     assert rel < 2e-2, f"dqkv rel err {rel}"
+
+
+@pytest.mark.parametrize("variant", [0, 11, 15], ids=["plain", "prescale_defer", "dma_dbuf"])
+def test_flash_fwd_variants_match_reference(variant):
+    from tensorhive_fixed_amd.ops.attention import flash_fwd
+    torch.manual_seed(2)
+    B, S, Hq, Hkv, D = 2, 328, 8, 2, 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    o, _ = flash_fwd(qkv, B, S, Hq, Hkv, D, variant=variant)
+    ref = _ref(qkv.float(), B, S, Hq, Hkv, D)
+    assert (o.float() - ref).abs().max().item() < 2e-2
