@@ -748,20 +748,17 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
 // fused kernel; paired roles that each recompute S = -9 %; LDS double-buffering = no change.)
 constexpr int C_BK = 128, C_BQ = 64, KC_TILE = 2 * C_BQ * 256 + 2 * C_BQ * 4;
 
-template <bool DK>
+template <bool DK, bool DMA>
 __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
                                         const float* __restrict__ LSE, const float* __restrict__ Dl,
                                         const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
                                         char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
                                         long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  char* qs = smem;
-  char* gs = smem + C_BQ * 256;
-  float* ls = reinterpret_cast<float*>(smem + 2 * C_BQ * 256);
-  float* ds = ls + C_BQ;
   // role-local thread id: waves 0-3 are the dK role, 4-7 the dV role of the same 128 keys
   const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-  // P exchange of wave pair w: [half][4 x float4][lane], 8 KB
-  float4v* pbuf = reinterpret_cast<float4v*>(smem + KC_TILE + w * 8192);
+  // tile buffers [Q | dO | lse | delta] (two with DMA), then the P exchange of wave pair w:
+  // [half][4 x float4][lane], 8 KB
+  float4v* pbuf = reinterpret_cast<float4v*>(smem + (DMA ? 2 : 1) * KC_TILE + w * 8192);
   const int k0 = kblk0 + 32 * w;
   const int key = k0 + c32;
   // dK role: V fragments (dP = dO V^T); dV role: K fragments (S = Q K^T)
@@ -798,19 +795,88 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
       dr = qq < S ? dr : 0.f;
     }
   };
-  if (total > 0) prefetch(0, 0);
-  for (int it = 0; it < total; ++it) {
-    __syncthreads();
-    stage_store<4>(DK ? qs : gs, xr, tid);
-    if (DK && tid < C_BQ) {
-      ls[tid] = lr * LOG2E;
-      ds[tid] = dr;
+  // DMA mode: the role's 4 waves DMA its 16 KB image (Q for dK, dO for dV) one tile ahead into
+  // the other buffer; lse / delta still go through registers, loaded two tiles ahead
+  unsigned rc[4];
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto dma_tile = [&](int h_i, int t_i, int buf) {
+    const int hq = hk * G + h_i;
+    const int qq0 = (qt0 + t_i) * C_BQ;
+    const ushort* base = DK ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
+    const long ldx = DK ? ld : ldo;
+    const unsigned img = lds0 + buf * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 4096;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
+      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
     }
-    __syncthreads();
+  };
+  // raw loads only: the row-validity selects happen in write_ld, so nothing consumes the loaded
+  // values right after their issue (a use there would make the compiler wait -- and the hardware
+  // vmcnt also counts the tile DMA issued just before)
+  int lq = 0;
+  auto load_ld = [&](int h_i, int t_i) {
+    if (DK && tid < C_BQ) {
+      const int hq = hk * G + h_i;
+      lq = (qt0 + t_i) * C_BQ + tid;
+      const long st = ((long)b * Hq + hq) * S;
+      const int qc = min(lq, S - 1);
+      lr = LSE[st + qc];
+      dr = Dl[st + qc];
+    }
+  };
+  auto write_ld = [&](int buf) {
+    if (DK && tid < C_BQ) {
+      float* l = reinterpret_cast<float*>(smem + buf * KC_TILE + 2 * C_BQ * 256);
+      l[tid] = DMA ? (lq < S ? lr * LOG2E : INFINITY) : lr * LOG2E;  // rows past S: P = 0 exactly
+      l[C_BQ + tid] = DMA ? (lq < S ? dr : 0.f) : dr;
+    }
+  };
+  int lh = 0, lt = 0;  // tile of the lse / delta registers (DMA mode)
+  auto adv = [&](int& hh, int& tt) {
+    if (++tt == per_head) { tt = 0; ++hh; }
+  };
+  if (DMA) {
+    // retire the K/V fragment loads with a wait the compiler sees (see the dQ kernel)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rc[u] = img_rc(wu * 4096 + u * 1024 + lane * 16);
+    if (total > 0) {
+      load_ld(0, 0);
+      write_ld(0);
+      dma_tile(0, 0, 0);
+      adv(lh, lt);
+      if (total > 1) load_ld(lh, lt);
+    }
+  } else if (total > 0) {
+    prefetch(0, 0);
+  }
+  for (int it = 0; it < total; ++it) {
+    char* cur = smem + (DMA ? (it & 1) * KC_TILE : 0);
+    if (DMA) {
+      wait_dma_barrier();  // tile it landed; every wave is past tile it-1 (its buffer is free)
+      if (it + 1 < total) {
+        write_ld((it + 1) & 1);  // before the DMA issue: the compiler's wait for lr/dr stays cheap
+        adv(pf_h, pf_t);
+        dma_tile(pf_h, pf_t, (it + 1) & 1);
+        adv(lh, lt);
+        if (it + 2 < total) load_ld(lh, lt);
+      }
+    } else {
+      __syncthreads();
+      stage_store<4>(DK ? cur : cur + C_BQ * 256, xr, tid);
+      write_ld(0);
+      __syncthreads();
+      if (++pf_t == per_head) { pf_t = 0; ++pf_h; }
+      if (it + 1 < total) prefetch(pf_h, pf_t);
+    }
+    const char* qs = cur;
+    const char* gs = cur + C_BQ * 256;
+    const float* ls = reinterpret_cast<const float*>(cur + 2 * C_BQ * 256);
+    const float* ds = ls + C_BQ;
     const int qbase = (qt0 + cur_t) * C_BQ;
     if (++cur_t == per_head) cur_t = 0;
-    if (++pf_t == per_head) { pf_t = 0; ++pf_h; }
-    if (it + 1 < total) prefetch(pf_h, pf_t);
     // phase 1 (both 32-query halves): dK role dP = dO V^T, dV role S = Q K^T -> P (to LDS)
     f32x16 c[2];
 #pragma unroll
@@ -850,7 +916,10 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
         }
       }
     }
-    __syncthreads();  // P of every pair visible
+    if (DMA)  // P of every pair visible (no vmcnt wait: the next tile's DMA stays in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      __syncthreads();
     // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -899,12 +968,13 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
   }
 }
 
+template <bool DMA>
 __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
     long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(16))) char smem[KC_TILE + 4 * 8192];  // tile | P exchange
+  __shared__ __attribute__((aligned(1024))) char smem[(DMA ? 2 : 1) * KC_TILE + 4 * 8192];  // tile(s) | P exchange
   const int nkb = (S + C_BK - 1) / C_BK;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   // (batch, kv head)-major: the key blocks of one group run together on an XCD and share its
@@ -917,10 +987,10 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
   const ushort* Vb = V + b * bs + (long)hk * HD;
   // wave-uniform role split; both roles pass the same barriers (same tile sequence)
   if (threadIdx.x >= 256)
-    kc_body<false>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+    kc_body<false, DMA>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
                    scale_log2, causal);
   else
-    kc_body<true>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+    kc_body<true, DMA>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
                   scale_log2, causal);
 }
 
@@ -992,9 +1062,16 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernel)
   if (!(flags & 8)) {
     const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;
-    fa_bwd_kc_kernel<<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                   (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv, B,
-                                                   S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+    if (dq_dma && !(flags & 64))  // same 32-bit offset bound; bit5 or bit6: register staging here
+      fa_bwd_kc_kernel<true><<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                           (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
+                                                           B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
+                                                           causal);
+    else
+      fa_bwd_kc_kernel<false><<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                            (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
+                                                            B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
+                                                            causal);
     TH_CHECK_LAUNCH();
   }
   const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;
