@@ -27,7 +27,7 @@ from ..ops.cross_entropy import linear_cross_entropy
 from ..ops.embedding import embedding
 from ..ops.linear import linear
 from ..ops.mlp import gate_up_swiglu
-from ..ops.rmsnorm import rmsnorm, rmsnorm_fork
+from ..ops.rmsnorm import rmsnorm, rmsnorm_add_fork, rmsnorm_fork
 from ..ops.swiglu import swiglu
 
 
@@ -87,6 +87,10 @@ WGRAD_TN = set(filter(None, os.environ.get("TH_WGRAD_TN_LAYERS", "wqkv,wo,w2").s
 _FORK = os.environ.get("TH_RMSNORM_FORK", "1") == "1"
 
 
+# residual adds fused into the following RMSNorm (rmsnorm_add_fork) instead of beta=1 GEMM epilogues
+ADD_NORM = _FORK and os.environ.get("TH_ADD_NORM", "1") == "1"
+
+
 def _norm(x, w, eps):
     if _FORK:
         return rmsnorm_fork(x, w, eps)
@@ -106,18 +110,30 @@ class LlamaBlock(nn.Module):
         self.w13 = nn.Parameter(torch.empty(2 * cfg.ffn_dim, d, device=device, dtype=dtype))
         self.w2 = nn.Parameter(torch.empty(d, cfg.ffn_dim, device=device, dtype=dtype))
 
-    def forward(self, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, B: int, S: int, pending: torch.Tensor | None = None):
+        """Without ADD_NORM: returns the block output.  With it: returns ``(y, x)``, the MLP-down
+        projection and the residual stream, whose sum the next norm forms (``pending`` of the next
+        block / the final norm)."""
         c = self.cfg
         # rmsnorm_fork: the residual gradient is added inside the RMSNorm backward kernel
-        h, x = _norm(x, self.attn_norm, c.norm_eps)
+        if pending is not None:
+            h, x = rmsnorm_add_fork(pending, x, self.attn_norm, c.norm_eps)
+        else:
+            h, x = _norm(x, self.attn_norm, c.norm_eps)
         qkv = linear(h, self.wqkv, wgrad_nt="wqkv" in WGRAD_NT, wgrad_tn="wqkv" in WGRAD_TN)
         o = qkv_attention(qkv, B, S, c.n_heads, c.n_kv_heads, c.head_dim, c.rope_theta)
-        x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT, wgrad_tn="wo" in WGRAD_TN)
-        h, x = _norm(x, self.ffn_norm, c.norm_eps)
+        if ADD_NORM:
+            y = linear(o, self.wo, wgrad_nt="wo" in WGRAD_NT, wgrad_tn="wo" in WGRAD_TN)
+            h, x = rmsnorm_add_fork(y, x, self.ffn_norm, c.norm_eps)
+        else:
+            x = linear(o, self.wo, residual=x, wgrad_nt="wo" in WGRAD_NT, wgrad_tn="wo" in WGRAD_TN)
+            h, x = _norm(x, self.ffn_norm, c.norm_eps)
         if "w13" in WGRAD_NT:  # fused gate|up + SwiGLU node: transposed dGU from the SwiGLU kernel
             a = gate_up_swiglu(h, self.w13)
         else:
             a = swiglu(linear(h, self.w13))
+        if ADD_NORM:
+            return linear(a, self.w2, wgrad_nt="w2" in WGRAD_NT, wgrad_tn="w2" in WGRAD_TN), x
         return linear(a, self.w2, residual=x, wgrad_nt="w2" in WGRAD_NT, wgrad_tn="w2" in WGRAD_TN)
 
 
@@ -165,12 +181,18 @@ class Llama(nn.Module):
         if gate is not None:
             gate(self.tok_emb)
         x = embedding(tokens, self.tok_emb).view(B * S, self.cfg.dim)
+        pending = None
         for blk in self.layers:
             if gate is not None:
                 gate(blk.attn_norm, blk.wqkv, blk.wo, blk.ffn_norm, blk.w13, blk.w2)
-            x = blk(x, B, S)
+            if ADD_NORM:
+                pending, x = blk(x, B, S, pending)
+            else:
+                x = blk(x, B, S)
         if gate is not None:
             gate(self.norm, self.lm_head)
+        if pending is not None:
+            return rmsnorm_add_fork(pending, x, self.norm, self.cfg.norm_eps)[0]
         return rmsnorm(x, self.norm, self.cfg.norm_eps)
 
     def forward(self, tokens: torch.Tensor, targets: torch.Tensor | None = None,

@@ -31,6 +31,7 @@ F = C.c_float
 # name -> argtypes (every function returns int: 0 = ok, <0 = rejected shape, >0 = hipError)
 _SIGS: dict[str, list] = {
     "th_rmsnorm_fwd": [P, P, P, P, I, I, F, P],
+    "th_rmsnorm_add_fwd": [P, P, P, P, P, P, I, I, F, P],
     "th_rmsnorm_bwd": [P, P, P, P, P, P, P, I, I, I, I, P, P],
     "th_swiglu_fwd": [P, P, L, I, P],
     "th_swiglu_bwd": [P, P, P, L, I, P],

@@ -8,12 +8,17 @@
 // registers, writes one f32 slab, and a second kernel sums the slabs (deterministic).
 #include "th_common.h"
 
-template <int MAXV>
+// ADD: x + addend is formed (rounded to bf16, as a GEMM epilogue would), written to xsum (the
+// residual stream) and normalised -- the residual add of the attention-out / MLP-down projections
+// fused into the next norm instead of a copy + beta=1 GEMM epilogue.
+template <int MAXV, bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const ushort* __restrict__ x,
-                                                          const ushort* __restrict__ w,
-                                                          ushort* __restrict__ y,
-                                                          float* __restrict__ rstd_out, int D,
-                                                          float eps) {
+                                                              const ushort* __restrict__ addend,
+                                                              ushort* __restrict__ xsum,
+                                                              const ushort* __restrict__ w,
+                                                              ushort* __restrict__ y,
+                                                              float* __restrict__ rstd_out, int D,
+                                                              float eps) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int nvec = D >> 3;
@@ -25,6 +30,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const ushort* __restri
     const int v = threadIdx.x + i * blockDim.x;
     if (v < nvec) {
       cache[i] = xr[v];
+      if (ADD) {
+        const ushort8 a = reinterpret_cast<const ushort8*>(addend + (size_t)row * D)[v];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cache[i][j] = f2bf(bf2f(cache[i][j]) + bf2f(a[j]));
+        reinterpret_cast<ushort8*>(xsum + (size_t)row * D)[v] = cache[i];
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float f = bf2f(cache[i][j]);
@@ -160,13 +171,34 @@ extern "C" int th_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd
   const int mv = pick_maxv(D, 256);
   dim3 g(T), b(256);
   if (mv <= 2)
-    rmsnorm_fwd_kernel<2><<<g, b, 0, s>>>((const ushort*)x, (const ushort*)w, (ushort*)y, rstd, D, eps);
+    rmsnorm_fwd_kernel<2, false><<<g, b, 0, s>>>((const ushort*)x, nullptr, nullptr, (const ushort*)w, (ushort*)y, rstd, D, eps);
   else if (mv <= 4)
-    rmsnorm_fwd_kernel<4><<<g, b, 0, s>>>((const ushort*)x, (const ushort*)w, (ushort*)y, rstd, D, eps);
+    rmsnorm_fwd_kernel<4, false><<<g, b, 0, s>>>((const ushort*)x, nullptr, nullptr, (const ushort*)w, (ushort*)y, rstd, D, eps);
   else if (mv <= 8)
-    rmsnorm_fwd_kernel<8><<<g, b, 0, s>>>((const ushort*)x, (const ushort*)w, (ushort*)y, rstd, D, eps);
+    rmsnorm_fwd_kernel<8, false><<<g, b, 0, s>>>((const ushort*)x, nullptr, nullptr, (const ushort*)w, (ushort*)y, rstd, D, eps);
   else
     return -2;
+  TH_CHECK_LAUNCH();
+}
+
+// xsum = x + addend (bf16), y = rmsnorm(xsum) * w
+extern "C" int th_rmsnorm_add_fwd(const void* x, const void* addend, const void* w, void* xsum, void* y,
+                                  float* rstd, int T, int D, float eps, hipStream_t s) {
+  if (D % 8 != 0 || T <= 0) return -1;
+  const int mv = pick_maxv(D, 256);
+  dim3 g(T), b(256);
+#define TH_RMS_ADD(MV)                                                                                   \
+  rmsnorm_fwd_kernel<MV, true><<<g, b, 0, s>>>((const ushort*)x, (const ushort*)addend, (ushort*)xsum, \
+                                               (const ushort*)w, (ushort*)y, rstd, D, eps)
+  if (mv <= 2)
+    TH_RMS_ADD(2);
+  else if (mv <= 4)
+    TH_RMS_ADD(4);
+  else if (mv <= 8)
+    TH_RMS_ADD(8);
+  else
+    return -2;
+#undef TH_RMS_ADD
   TH_CHECK_LAUNCH();
 }
 

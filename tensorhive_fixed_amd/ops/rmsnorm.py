@@ -37,6 +37,29 @@ def _fwd(x: torch.Tensor, w: torch.Tensor, eps: float):
     return x2, y, rstd
 
 
+def _fwd_add(y: torch.Tensor, r: torch.Tensor, w: torch.Tensor, eps: float):
+    """xsum = y + r (bf16-rounded, as a beta=1 GEMM epilogue would produce), h = rmsnorm(xsum)."""
+    D = y.shape[-1]
+    y2, r2 = y.reshape(-1, D), r.reshape(-1, D)
+    if not y2.is_contiguous():
+        y2 = y2.contiguous()
+    if not r2.is_contiguous():
+        r2 = r2.contiguous()
+    T = y2.shape[0]
+    if y2.is_cuda:
+        if y2.dtype != torch.bfloat16 or r2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or D % 8:
+            raise ValueError("rmsnorm_add kernel needs bf16 [T, D] inputs, bf16 [D] weight, D % 8 == 0")
+        xsum = torch.empty_like(y2)
+        h = torch.empty_like(y2)
+        rstd = torch.empty(T, device=y2.device, dtype=torch.float32)
+        _lib.call("th_rmsnorm_add_fwd", y2.data_ptr(), r2.data_ptr(), w.data_ptr(), xsum.data_ptr(), h.data_ptr(),
+                  rstd.data_ptr(), T, D, float(eps), _lib.stream_ptr(y2.device))
+        return xsum, h, rstd
+    xsum = (y2.float() + r2.float()).to(y2.dtype)
+    x2, h, rstd = _fwd(xsum, w, eps)
+    return x2, h, rstd
+
+
 def _bwd(x2, w, rstd, dy: torch.Tensor, dres: torch.Tensor | None, shape):
     """dx (+ dres, fused on the GPU) and the routed weight gradient."""
     T, D = x2.shape
@@ -115,6 +138,33 @@ class _RMSNormFork(torch.autograd.Function):
         x2, w, rstd = ctx.saved_tensors
         dx, gw = _bwd(x2, w, rstd, dy, dres, ctx.shape)
         return dx, gw, None
+
+
+class _RMSNormAddFork(torch.autograd.Function):
+    """``(rmsnorm(y + r), y + r)``: the residual add of the previous sublayer fused into this norm
+    (one kernel reads y and r, writes the residual stream and the normalised output), replacing the
+    beta=1 GEMM epilogue whose input copy cost a full [T, D] read + write per residual.  Both
+    inputs receive the same gradient: the norm backward with the residual-branch gradient added."""
+
+    @staticmethod
+    def forward(ctx, y: torch.Tensor, r: torch.Tensor, w: torch.Tensor, eps: float):
+        xsum, h, rstd = _fwd_add(y, r, w, eps)
+        ctx.save_for_backward(xsum, w, rstd)
+        ctx.shape = y.shape
+        return h.view(y.shape), xsum.view(y.shape)
+
+    @staticmethod
+    def backward(ctx, dh: torch.Tensor, dres: torch.Tensor | None):
+        xsum, w, rstd = ctx.saved_tensors
+        dx, gw = _bwd(xsum, w, rstd, dh, dres, ctx.shape)
+        return dx, dx, gw, None
+
+
+def rmsnorm_add_fork(y: torch.Tensor, r: torch.Tensor, w: torch.Tensor,
+                     eps: float = 1e-5) -> tuple[torch.Tensor, torch.Tensor]:
+    """``h, x = rmsnorm_add_fork(y, r, w)`` with ``x = y + r``: use ``h`` for the sublayer and ``x``
+    as the residual stream."""
+    return _RMSNormAddFork.apply(y, r, w, eps)
 
 
 def rmsnorm_fork(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> tuple[torch.Tensor, torch.Tensor]:

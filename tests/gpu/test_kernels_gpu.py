@@ -240,3 +240,27 @@ def test_rmsnorm_fork_fuses_residual_gradient():
     _close(x.grad, xf.grad, 5e-2, 1e-2)
     _close(w.grad, wf.grad, 0.5, 1e-2)
     assert rmsnorm is not None
+
+
+def test_rmsnorm_add_fork_kernel_matches_fp32_reference():
+    from tensorhive_fixed_amd.ops.rmsnorm import rmsnorm_add_fork
+    torch.manual_seed(3)
+    T, D = 300, 4096
+    y = torch.randn(T, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(T, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(D, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    h, x = rmsnorm_add_fork(y, r, w)
+    s = y.detach().float() + r.detach().float()
+    assert (x.float() - s).abs().max().item() < 0.07  # bf16 rounding of the sum
+    xs = x.detach().float()
+    ref = xs * torch.rsqrt(xs.pow(2).mean(-1, keepdim=True) + 1e-5) * w.detach().float()
+    assert (h.float() - ref).abs().max().item() < 0.05
+    dh, dx = torch.randn_like(h), torch.randn_like(x)
+    torch.autograd.backward([h, x], [dh, dx])
+    xr = xs.clone().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    hr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    torch.autograd.backward([hr, xr], [dh.float(), dx.float()])
+    for a, b in ((y.grad, xr.grad), (r.grad, xr.grad)):
+        assert ((a.float() - b).norm() / b.norm()).item() < 1e-2
+    assert ((w.grad.float() - wr.grad).norm() / wr.grad.norm()).item() < 1e-2
