@@ -21,6 +21,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from datetime import timedelta
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -109,11 +110,30 @@ def _headers(u) -> dict:
     return {"Authorization": "Bearer " + auth.create_access_token(u.id, u.role_names, fresh=True)}
 
 
+def _lat_stats(lat: list[float], requests: int) -> dict:
+    return {"p50_ms": round(_pct(lat, 0.5), 3), "p99_ms": round(_pct(lat, 0.99), 3),
+            "mean_ms": round(statistics.fmean(lat), 3), "requests": requests}
+
+
 def poll_latency(requests: int = 1000, nodes: int = 8, gpus: int = 8, warmup: int = 20) -> dict:
-    """p50/p99 of the dashboard poll on ``nodes`` x ``gpus`` simulated GPUs."""
+    """p50/p99 of the dashboard poll on ``nodes`` x ``gpus`` simulated GPUs, three ways:
+
+    * ``admin_inprocess`` -- Flask test client, admin (no permission filter);
+    * ``user_inprocess`` -- Flask test client, an ordinary user whose restrictions cover half of
+      every node's GPUs (per-resource restrictions, so every poll runs the user lookup and
+      ``filter_infrastructure_by_user_restrictions``, reference ``controllers/nodes.py:13-50``);
+    * ``user_socket`` -- the same user over HTTP/1.1 keep-alive to the threaded WSGI server the
+      daemon runs (``api/app.py``), i.e. what a browser pays minus the network."""
+    import http.client
+    import threading
+
+    from werkzeug.serving import make_server
+
     from .api.app import create_app
     from .core.daemon import Daemon
     from .core.telemetry import StubBackend
+    from .models.orm import Resource, Restriction, Role, User
+    from .utils import dates
 
     hosts = {f"mi355x-{i:02d}": "fake" for i in range(nodes)}
     with sandbox(hosts, stub_gpus=gpus) as (cfg, _d):
@@ -121,22 +141,62 @@ def poll_latency(requests: int = 1000, nodes: int = 8, gpus: int = 8, warmup: in
         daemon = Daemon(cfg, backends={h: stub for h in hosts}, init_key=False, test_ssh=False)
         for h in hosts:
             daemon.infrastructure.publish(h, stub.sample(h))
-        client = create_app(daemon).test_client()
-        hdr = _headers(_admin())
+        app = create_app(daemon)
+        client = app.test_client()
+        admin = _admin()
+        user = User(username="alice", password="benchmark password", email="alice@example.org",
+                    roles=[Role(name="user")])
+        user.save()
+        r = Restriction(name="half", starts_at=dates.utcnow() - timedelta(days=1), is_global=False)
+        r.save()
+        r.apply_to_user(user)
+        for h in hosts:
+            for i in range(0, gpus, 2):
+                res = Resource(id=stub.gpu_uuid(h, i), name="MI355X", hostname=h)
+                res.save()
+                r.apply_to_resource(res)
+        client.get("/api/nodes/metrics", headers=_headers(admin))  # registers every GPU resource once
         out = {}
-        for path in ("/api/nodes/metrics", "/api/nodes/mi355x-00/gpu/metrics?metric_type=utilization"):
-            lat = []
-            for i in range(warmup + requests):
-                t0 = time.perf_counter()
-                r = client.get(path, headers=hdr)
-                dt = (time.perf_counter() - t0) * 1e3
-                assert r.status_code == 200, r.data[:200]
-                if i >= warmup:
-                    lat.append(dt)
-            out[path] = {"p50_ms": round(_pct(lat, 0.5), 3), "p99_ms": round(_pct(lat, 0.99), 3),
-                         "mean_ms": round(statistics.fmean(lat), 3), "requests": requests}
-        daemon.shutdown()
-        return {"metric": "dashboard_poll_latency", "nodes": nodes, "gpus_per_node": gpus, "results": out}
+        paths = ("/api/nodes/metrics", "/api/nodes/mi355x-00/gpu/metrics?metric_type=utilization")
+        for label, who in (("admin_inprocess", admin), ("user_inprocess", user)):
+            hdr = _headers(who)
+            for path in paths:
+                lat = []
+                for i in range(warmup + requests):
+                    t0 = time.perf_counter()
+                    resp = client.get(path, headers=hdr)
+                    dt = (time.perf_counter() - t0) * 1e3
+                    assert resp.status_code == 200, resp.data[:200]
+                    if i >= warmup:
+                        lat.append(dt)
+                out.setdefault(label, {})[path] = _lat_stats(lat, requests)
+        # the user's view really is filtered: half of each node's GPUs
+        seen = client.get("/api/nodes/metrics", headers=_headers(user)).get_json()
+        visible = sum(len(v.get("GPU") or {}) for v in seen.values())
+        srv = make_server("127.0.0.1", 0, app, threaded=True)
+        th = threading.Thread(target=srv.serve_forever, daemon=True)
+        th.start()
+        try:
+            conn = http.client.HTTPConnection("127.0.0.1", srv.server_port, timeout=10)
+            hdr = _headers(user)
+            for path in paths:
+                lat = []
+                for i in range(warmup + requests):
+                    t0 = time.perf_counter()
+                    conn.request("GET", path, headers=hdr)
+                    resp = conn.getresponse()
+                    body = resp.read()
+                    dt = (time.perf_counter() - t0) * 1e3
+                    assert resp.status == 200, body[:200]
+                    if i >= warmup:
+                        lat.append(dt)
+                out.setdefault("user_socket", {})[path] = _lat_stats(lat, requests)
+            conn.close()
+        finally:
+            srv.shutdown()
+            daemon.shutdown()
+        return {"metric": "dashboard_poll_latency", "nodes": nodes, "gpus_per_node": gpus,
+                "user_visible_gpus": visible, "results": out}
 
 
 def launch_latency(trials: int = 5, command: str = "echo started; sleep 2") -> dict:
@@ -279,6 +339,133 @@ def scheduled_training(gpus: int = 1, steps: int = 10, warmup: int = 2, micro_ba
         return {"metric": "scheduled_llama3_ddp_tokens_per_sec", "gpus": gpus, "micro_batch": micro_batch,
                 "steps_logged": len(rates), "tokens_per_sec": round(statistics.fmean(steady), 1) if steady else None,
                 "completed": done, "wall_s": round(time.time() - t0, 1), "log_tail": lines[-3:]}
+
+
+def multitenant(jobs_per_user: int = 8, seed: int = 0, duration_s: tuple[float, float] = (0.4, 1.2),
+                arrival_s: float = 0.15, pinned: bool = False) -> dict:
+    """BASELINE config 4 on a simulated 8-GPU MI355X node (scaled time): three users with
+    overlapping reservations submit two-GPU jobs to the queue; the real scheduler and monitoring
+    threads place and start them.  Reports queue wait (enqueue -> running) p50/p99, node GPU
+    utilisation over the run and while jobs were waiting, and the violation path (a foreign
+    process on a reserved GPU is detected and walled on the intruder's terminal).
+
+    ``pinned=True`` is the reference's model: every job names its device pair up front
+    (each user has a favourite pair), so a job waits for THAT pair even when others are free.
+    The default lets the allocator pick any free, permitted pair (``HIP_VISIBLE_DEVICES=auto:2``)."""
+    import random
+
+    from .core.daemon import Daemon
+    from .core.services import JobSchedulingService, MonitoringService, ProtectionService
+    from .core.telemetry import StubBackend
+    from .core.violation_handlers import MessageSendingBehaviour, ProtectionHandler
+    from .models.orm import (CommandSegment, Job, JobStatus, Reservation, Resource, Restriction, Role,
+                             SegmentType, Task, User)
+    from .utils import dates
+
+    rng = random.Random(seed)
+    host = "mi355x-00"
+    with sandbox({host: "simulated"}, job_interval=3600.0) as (cfg, _d):
+        stub = StubBackend(gpus_per_host=8)
+        daemon = Daemon(cfg, backends={host: stub}, init_key=False, test_ssh=False)
+        node = daemon.transports.get(host)
+        daemon.infrastructure.publish(host, stub.sample(host))
+        uuids = [stub.gpu_uuid(host, i) for i in range(8)]
+        for u in uuids:
+            Resource(id=u, name="MI355X", hostname=host).save()
+        names = ("alice", "bob", "carol")
+        users = {}
+        g = Restriction(name="everyone", starts_at=dates.utcnow() - timedelta(days=1), is_global=True)
+        g.save()
+        for n in names:
+            users[n] = User(username=n, password="benchmark password", email=f"{n}@example.org",
+                            roles=[Role(name="user")])
+            users[n].save()
+            g.apply_to_user(users[n])
+        now = dates.utcnow()
+        for n, gpus, start in (("alice", (0, 1), now - timedelta(minutes=5)), ("bob", (2, 3), now - timedelta(minutes=5)),
+                               ("carol", (4,), now + timedelta(minutes=10))):
+            for i in gpus:
+                Reservation(user_id=users[n].id, title=f"{n}-{i}", description="", resource_id=uuids[i],
+                            start=start, end=start + timedelta(hours=2)).save()
+        favourite = {"alice": "0,1", "bob": "2,3", "carol": "6,7"}
+        seg = CommandSegment(name="HIP_VISIBLE_DEVICES", segment_type=SegmentType.env_variable)
+        seg.save()
+        plan = []  # (arrival offset, user, duration)
+        t = 0.0
+        for k in range(jobs_per_user * len(names)):
+            t += rng.expovariate(1.0 / arrival_s)
+            plan.append((t, names[k % len(names)], rng.uniform(*duration_s)))
+        mon = MonitoringService(0.02, {host: stub})
+        sched = JobSchedulingService(0.25, 5, 30)
+        daemon.add_service(mon)
+        daemon.add_service(sched)
+        mon.start()
+        sched.start()
+        enq: dict[int, float] = {}
+        dur: dict[int, float] = {}
+        started: dict[int, float] = {}
+        busy_samples, waiting_samples = [], []
+        violations = {}
+        from .database import db_session
+
+        t0 = time.time()
+        try:
+            pending = list(plan)
+            deadline = t0 + 120
+            while time.time() < deadline:
+                now_s = time.time() - t0
+                while pending and pending[0][0] <= now_s:
+                    _at, n, d = pending.pop(0)
+                    j = Job(name=f"{n}-{len(enq)}", description="", user_id=users[n].id)
+                    j.save()
+                    tk = Task(command="python train.py", hostname=host)
+                    tk.save()
+                    tk.add_cmd_segment(seg, favourite[n] if pinned else "auto:2")
+                    j.add_task(tk)
+                    j.enqueue()
+                    enq[j.id], dur[j.id] = time.time(), d
+                    daemon.wake("enqueue")
+                for jid, ts in list(sched.launch_log):
+                    started.setdefault(jid, ts)
+                db_session.expire_all()
+                for jid, ts in started.items():  # finish jobs whose time is up
+                    if dur.get(jid) is not None and time.time() - ts >= dur[jid]:
+                        for tk in Job.get(jid).tasks:
+                            if tk.pid:
+                                node.exit_task(tk.pid)
+                        dur[jid] = None
+                        daemon.wake("exit")
+                sample = stub.sample(host)["GPU"]
+                busy_samples.append(sum(1 for x in sample.values() if x["processes"]))
+                waiting_samples.append(any(j not in started for j in enq))
+                if not violations and now_s > 1.0:  # a foreign process on bob's reserved GPU 2
+                    stub.add_process(host, 2, 66666, "mallory")
+                    node.ttys = [("mallory", "pts/7")]
+                    mon.do_run()
+                    prot = ProtectionService(1.0, [ProtectionHandler(MessageSendingBehaviour(daemon.transports))], 1)
+                    prot.inject(daemon)
+                    prot.do_run()
+                    violations = {k: [r["OWNER_USERNAME"] for r in v["RESERVATIONS"]]
+                                  for k, v in prot.last_violations.items()}
+                    node._drop_gpu_process(66666)
+                if not pending and len(started) == len(enq) and all(v is None for v in dur.values()):
+                    break
+                time.sleep(0.01)
+            makespan = time.time() - t0
+        finally:
+            daemon.shutdown()
+        waits = [(started[j] - enq[j]) * 1e3 for j in enq if j in started]
+        util = statistics.fmean(busy_samples) / 8 if busy_samples else 0.0
+        contended = [b for b, w in zip(busy_samples, waiting_samples) if w]
+        return {"metric": "multitenant_queue", "policy": "pinned (reference)" if pinned else "auto:2 gang placement",
+                "jobs": len(enq), "completed": sum(1 for v in dur.values() if v is None),
+                "queue_wait_p50_ms": round(_pct(waits, 0.5), 1), "queue_wait_p99_ms": round(_pct(waits, 0.99), 1),
+                "node_gpu_util": round(util, 3),
+                "gpu_util_while_jobs_wait": round(statistics.fmean(contended) / 8, 3) if contended else None,
+                "makespan_s": round(makespan, 2), "violations": violations,
+                "walled_ttys": [t for t, _ in node.tty_messages],
+                "note": "simulated node (th-run protocol in-process), scaled time: job durations "
+                        f"{duration_s[0]}-{duration_s[1]} s, mean inter-arrival {arrival_s} s"}
 
 
 def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3) -> dict:

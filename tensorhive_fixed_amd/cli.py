@@ -6,7 +6,7 @@
     tensorhive key                                              print the authorized_keys line
     tensorhive create user [-m]                                 account prompt (repeat with -m)
     tensorhive doctor                                           ROCm / amdsmi / RCCL / xGMI checks (new)
-    tensorhive bench poll|launch|train|scheduled                N08 benchmark harnesses (new)
+    tensorhive bench poll|launch|train|scheduled|multitenant    N08 benchmark harnesses (new)
     tensorhive profile --task ID                                rocprofv3 wrapper line for a task (new)
 
 Fixes vs. the reference: ``init`` is a function the main command can call (the reference invoked
@@ -214,14 +214,18 @@ def doctor():
 
 
 @main.command()
-@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled"]))
+@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled", "multitenant"]))
 @click.option("--requests", default=1000)
 @click.option("--gpus", default=1)
-def bench(what, requests, gpus):
-    """Benchmarks of BASELINE.md: poll latency, queued-job launch latency, training tokens/s."""
+@click.option("--pinned", is_flag=True, help="multitenant: reference-style pinned device pairs")
+def bench(what, requests, gpus, pinned):
+    """Benchmarks of BASELINE.md: poll latency, queued-job launch latency, multi-tenant queue
+    wait / GPU utilisation, training tokens/s."""
     from . import benchmarks
 
-    if what == "poll":
+    if what == "multitenant":
+        click.echo(json.dumps(benchmarks.multitenant(pinned=pinned)))
+    elif what == "poll":
         click.echo(json.dumps(benchmarks.poll_latency(requests)))
     elif what == "launch":
         click.echo(json.dumps(benchmarks.launch_latency()))

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import logging
+import time
 
 from ..models.orm import Job, JobStatus, Task
 from ..utils.exceptions import ForbiddenException
@@ -138,43 +139,80 @@ def _fan_out(fn, items):
 
 
 @guarded(not_found="job.not_found")
-def business_execute(id: int):
-    from ..core import task_nursery
-    from ..models.orm import TaskStatus
+def business_execute(id: int, placements: dict | None = None, daemon=None):
+    """Claim devices for every task, then spawn them all in parallel.
 
+    Allocation (``core/allocation.py``) runs under the lock shared with the scheduler tick: the
+    running check, the device choice for ``auto:N`` tasks and the ``gpu_allocations`` insert
+    are one atomic step, so a double execute, or an execute racing a queue tick, gets 409
+    instead of a second process on the same GPU.  ``placements`` (task id -> [uuid]) carries
+    the scheduler's choices for ``auto`` tasks; they are re-validated under the lock."""
+    from ..core import allocation, task_nursery
+    from ..database import db_session
+    from ..models.orm import GpuAllocation, TaskStatus
+
+    d = daemon if daemon is not None else _daemon()
     job = Job.get(id)
-    if job.status is JobStatus.running:
-        return {"msg": M("job.execute.failure.state", reason="Job is already running")}, 409
     cache = task_ctl.SessionCache()
-    failed, todo = [], []
     for t in job.tasks:
         task_ctl.synchronize(t.id, cache)
-        if t.status is TaskStatus.running or not t.full_command or not t.hostname or job.user is None:
-            failed.append(t.id)
-            continue
-        todo.append((t, (t.full_command, t.hostname, job.user.username, str(t.id))))
-
-    def spawn(cmd, host, user, tid):
+    with allocation.ALLOC_LOCK:
+        db_session.expire_all()
+        job = Job.get(id)
+        if (job.status is JobStatus.running or job.id in allocation.launching
+                or GpuAllocation.query.filter(GpuAllocation.job_id == job.id).count()):
+            return {"msg": M("job.execute.failure.state", reason="Job is already running")}, 409
+        snapshot = d.infrastructure.snapshot().data if d is not None else {}
+        window = d.scheduling_window() if d is not None else None
         try:
-            return task_nursery.spawn(cmd, host, user, name_appendix=tid)
-        except Exception as e:  # noqa: BLE001
-            log.warning("spawn of task %s failed: %s", tid, e)
-            return None
+            plan = allocation.plan_job(job, snapshot, placements, **({"window": window} if window else {}))
+            allocation.claim(job, plan)
+        except allocation.AllocationError as e:
+            return {"msg": M("job.execute.failure.state", reason=e.reason)}, e.status
+        allocation.launching.add(job.id)
+    try:
+        failed, todo = [], []
+        for t in job.tasks:
+            if t.status is TaskStatus.running or not t.full_command or not t.hostname or job.user is None:
+                failed.append(t.id)
+                continue
+            devices = [i for i, _u in plan.get(t.id, [])]
+            cmd = allocation.render_command(t, devices)
+            todo.append((t, (cmd, t.hostname, job.user.username, str(t.id))))
 
-    pids = _fan_out(spawn, [args for _t, args in todo])
-    for (t, _args), pid in zip(todo, pids):
-        if pid is None:
-            failed.append(t.id)
-            continue
-        t.pid = pid
-        t.status = TaskStatus.running
-        t.save()
-    job.synchronize_status()
-    job.save()
+        def spawn(cmd, host, user, tid):
+            try:
+                return task_nursery.spawn(cmd, host, user, name_appendix=tid)
+            except Exception as e:  # noqa: BLE001
+                log.warning("spawn of task %s failed: %s", tid, e)
+                return None
+
+        pids = _fan_out(spawn, [args for _t, args in todo])
+        for (t, _args), pid in zip(todo, pids):
+            if pid is None:
+                failed.append(t.id)
+                continue
+            t.pid = pid
+            t.status = TaskStatus.running
+            t.save()
+        for tid in failed:
+            allocation.release_task(tid)
+        job.synchronize_status()
+        job.save()
+    finally:
+        with allocation.ALLOC_LOCK:
+            allocation.launching.discard(job.id)
+            allocation.launched_at[job.id] = time.monotonic()
     if failed:
         return {"msg": M("job.execute.failure.tasks", reason="Could not spawn some tasks"),
                 "not_spawned_list": failed}, 422
     return {"msg": M("job.execute.success"), "job": job.as_dict()}, 200
+
+
+def _daemon():
+    from ..api.app import daemon
+
+    return daemon()
 
 
 @guarded(not_found="job.not_found", assertion="job.enqueue.failure", assertion_status=409)
@@ -299,8 +337,16 @@ def _placements(form: dict) -> list[dict]:
     for p in form["placements"]:
         assert isinstance(p, dict) and isinstance(p.get("hostname"), str), "placement needs a hostname"
         gpus = p.get("gpus", [p["gpu"]] if "gpu" in p else [])
-        assert all(isinstance(g, int) and g >= 0 for g in gpus), "gpus must be device indices"
-        out.append({"hostname": p["hostname"], "gpus": gpus, "role": p.get("role", "worker")})
+        count = p.get("gpuCount")
+        if isinstance(gpus, str) and gpus.startswith("auto"):  # "auto:4": the scheduler picks
+            count = int(gpus.split(":", 1)[1]) if ":" in gpus else count
+            gpus = []
+        if count is not None:
+            assert isinstance(count, int) and count >= 1, "gpuCount must be a positive integer"
+            assert not gpus, "give either gpus or gpuCount"
+        else:
+            assert all(isinstance(g, int) and g >= 0 for g in gpus), "gpus must be device indices"
+        out.append({"hostname": p["hostname"], "gpus": gpus, "count": count, "role": p.get("role", "worker")})
     assert out, "no placements"
     return out
 
@@ -315,7 +361,8 @@ def generate_tasks(id: int, form: dict):
     host), ``torch`` (one task per GPU with explicit ``--rank``/``--world-size``), ``tf2``
     (TF_CONFIG per task, ports auto-increment per host from 2222; ``role`` chief/worker/ps/
     evaluator), ``tf1`` (ClusterSpec ``--ps_hosts/--worker_hosts``; ``role`` ps/worker).
-    ``placements``: ``[{"hostname": h, "gpus": [i, ...] | "gpu": i, "role": r}]``."""
+    ``placements``: ``[{"hostname": h, "gpus": [i, ...] | "gpu": i | "auto:N", "gpuCount": N, "role": r}]``;
+    a count (``torchrun`` only) leaves the choice of devices to the allocator at launch time."""
     from ..core import launcher
     from . import task as task_ctl
 
@@ -329,7 +376,7 @@ def generate_tasks(id: int, form: dict):
     master = pl[0]["hostname"]
     if kind == "torchrun":
         port = form.get("masterPort") or 29500
-        forms = [launcher.torchrun_task(p["hostname"], p["gpus"], master, port, nnodes=len(pl),
+        forms = [launcher.torchrun_task(p["hostname"], p["gpus"] or p["count"], master, port, nnodes=len(pl),
                                         module=form.get("module") or "tensorhive_fixed_amd.workloads.llama3_ddp")
                  for p in pl]
     elif kind == "torch":

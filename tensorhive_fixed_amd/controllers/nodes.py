@@ -8,7 +8,6 @@ read path).  Non-admins see only GPUs their restrictions allow.  Responses carry
 """
 from __future__ import annotations
 
-import copy
 import threading
 
 from flask import Response
@@ -53,24 +52,69 @@ def register_resources_from_snapshot(snap=None) -> None:
         _registered_version["v"] = snap.version
 
 
+def filtered_view(data: dict, allowed: set[str] | None) -> dict:
+    """The snapshot restricted to ``allowed`` GPU UUIDs (``None`` = everything), hosts left
+    without GPUs dropped (reference ``models/User.py:166-186``).  A shallow view: host and GPU
+    entries are shared with the immutable snapshot, never copied -- the reference deep-copied
+    the whole infrastructure on every poll (``controllers/nodes.py:15``)."""
+    if allowed is None:
+        return data
+    out = {}
+    for host, entry in data.items():
+        gpus = (entry or {}).get("GPU")
+        if gpus is None:
+            continue
+        keep = {u: g for u, g in gpus.items() if u in allowed}
+        if keep:
+            out[host] = {**entry, "GPU": keep}
+    return out
+
+
+def _allowed() -> set[str] | None:
+    return None if is_admin() else User.get(me()).allowed_gpu_uuids()
+
+
 def get_infrastructure() -> dict:
+    """Read-only view of the current snapshot as the caller may see it (do not mutate)."""
     snap = _snapshot()
     if snap is None:
         return {}
     register_resources_from_snapshot(snap)
-    infra = copy.deepcopy(snap.data)
-    if not is_admin():
-        user = User.get(me())
-        infra = user.filter_infrastructure_by_user_restrictions(infra)
-    return infra
+    return filtered_view(snap.data, _allowed())
 
 
-def _with_age(content, status=200):
+class _JsonCache:
+    """Serialised ``/nodes/metrics`` bodies keyed by (snapshot version, permitted GPU set): every
+    dashboard of the same permission class shares one ``json.dumps`` per sample."""
+
+    def __init__(self, size: int = 64):
+        self.size = size
+        self._d: dict = {}
+        self._lock = threading.Lock()
+
+    def get(self, key, build):
+        with self._lock:
+            hit = self._d.get(key)
+        if hit is not None:
+            return hit
+        body = build()
+        with self._lock:
+            if len(self._d) >= self.size:
+                self._d.pop(next(iter(self._d)))
+            self._d[key] = body
+        return body
+
+
+_metrics_cache = _JsonCache()
+
+
+def _with_age(content, status=200, body: str | None = None, snap=None):
     import json
     import time
 
-    snap = _snapshot()
-    resp = Response(json.dumps(content, default=str), status=status, mimetype="application/json")
+    snap = snap or _snapshot()
+    resp = Response(body if body is not None else json.dumps(content, default=str), status=status,
+                    mimetype="application/json")
     if snap is not None and snap.sampled_at:
         now = time.time()
         resp.headers["X-Sample-Age-Ms"] = str(int(1000 * (now - min(snap.sampled_at.values()))))
@@ -81,7 +125,16 @@ def _with_age(content, status=200):
 
 
 def get_all_data():
-    return _with_age(get_infrastructure())
+    import json
+
+    snap = _snapshot()
+    if snap is None:
+        return _with_age({})
+    register_resources_from_snapshot(snap)
+    allowed = _allowed()
+    key = (id(daemon()), snap.version, None if allowed is None else frozenset(allowed))
+    body = _metrics_cache.get(key, lambda: json.dumps(filtered_view(snap.data, allowed), default=str))
+    return _with_age(None, body=body, snap=snap)
 
 
 def get_hostnames():

@@ -14,10 +14,12 @@ not interpreted (north star: no CUDA paths).
 from __future__ import annotations
 
 import logging
+import time
 
 from sqlalchemy.exc import NoResultFound
 
-from ..core import task_nursery
+from ..core import allocation, task_nursery
+from ..database import db_session
 from ..core.scheduling import parse_device_list
 from ..models.orm import CommandSegment, Job, SegmentType, Task, TaskStatus
 from ._common import Abort, M, guarded, is_admin, me
@@ -26,14 +28,17 @@ log = logging.getLogger(__name__)
 
 
 class SessionCache:
-    """(host, user) -> set of live task pids, fetched lazily once."""
+    """(host, user) -> set of live task pids, fetched lazily once.  The monotonic time each list
+    was fetched is kept: a launch that finished after it is not judged by that list."""
 
     def __init__(self):
         self._d: dict[tuple[str, str], set[int] | Exception] = {}
+        self.fetched_at: dict[tuple[str, str], float] = {}
 
     def pids(self, host: str, user: str) -> set[int]:
         key = (host, user)
         if key not in self._d:
+            self.fetched_at[key] = time.monotonic()
             try:
                 self._d[key] = set(task_nursery.running_pids(host, user))
             except Exception as e:  # noqa: BLE001
@@ -45,6 +50,12 @@ class SessionCache:
 
 
 def synchronize(task_id: int, cache: SessionCache | None = None) -> None:
+    """Reconcile one task with the live sessions on its node.
+
+    The transition is decided under the allocation lock on a fresh read of the task, and is
+    skipped while the job is launching or when its launch finished after the session list was
+    fetched -- otherwise a stale view could erase a just-spawned pid and release the devices of
+    a running task (tests/test_allocation.py::test_concurrent_executes_and_ticks_never_double_allocate)."""
     cache = cache or SessionCache()
     try:
         task = Task.get(task_id)
@@ -55,21 +66,31 @@ def synchronize(task_id: int, cache: SessionCache | None = None) -> None:
         assert task.hostname, "hostname is empty"
         assert job is not None and job.user is not None, "user does not exist"
         live = cache.pids(task.hostname, job.user.username)
+        fetched = cache.fetched_at.get((task.hostname, job.user.username), 0.0)
     except Exception as e:  # noqa: BLE001 -- unreachable node, bad config, ...
         log.debug("task %s unsynchronized: %s", task_id, e)
         task.status = TaskStatus.unsynchronized
         task.save()
         return
-    if task.pid is None or task.pid not in live:
-        if task.status is TaskStatus.running:
-            task.status = TaskStatus.terminated
-        elif task.status is TaskStatus.unsynchronized:
-            task.status = TaskStatus.not_running
-        task.pid = None
-        task.save()
-    elif task.status is not TaskStatus.running:
-        task.status = TaskStatus.running  # re-adopt a live session after a daemon restart
-        task.save()
+    with allocation.ALLOC_LOCK:
+        try:
+            db_session.refresh(task)
+        except Exception:  # noqa: BLE001 -- deleted meanwhile
+            db_session.rollback()
+            return
+        if task.job_id in allocation.launching or allocation.launched_at.get(task.job_id, -1.0) >= fetched:
+            return
+        if task.pid is None or task.pid not in live:
+            if task.status is TaskStatus.running:
+                task.status = TaskStatus.terminated
+            elif task.status is TaskStatus.unsynchronized:
+                task.status = TaskStatus.not_running
+            task.pid = None
+            task.save()
+            allocation.release_task(task.id)  # the task's devices are free again
+        elif task.status is not TaskStatus.running:
+            task.status = TaskStatus.running  # re-adopt a live session after a daemon restart
+            task.save()
 
 
 def parse_gpu_id_from_command(value: str | None) -> int | None:

@@ -141,6 +141,13 @@ class Daemon:
         if s is not None:
             s.wake()
 
+    def scheduling_window(self):
+        """How long a GPU must stay free before a queued job may take it
+        (``schedule_queued_jobs_when_free_mins``); also the look-ahead of device placement."""
+        from datetime import timedelta
+
+        return timedelta(minutes=self.cfg.job_scheduling.schedule_queued_jobs_when_free_mins)
+
     # ------------------------------------------------------------------ introspection
     def topology(self) -> dict:
         out = {}

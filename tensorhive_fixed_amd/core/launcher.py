@@ -86,14 +86,20 @@ def hip_visible_devices(indices: list[int]) -> str:
 
 
 # --------------------------------------------------------------------------- builders
-def torchrun_task(host: str, gpu_indices: list[int], master_host: str, master_port: int = 29500,
+def torchrun_task(host: str, gpu_indices: list[int] | int, master_host: str, master_port: int = 29500,
                   nnodes: int = 1, module: str = "tensorhive_fixed_amd.workloads.llama3_ddp",
                   script_args: list[tuple[str, str]] | None = None) -> dict:
-    """A TaskForm body for one node of a torchrun job."""
-    envs = [{"name": "HIP_VISIBLE_DEVICES", "value": hip_visible_devices(gpu_indices)}]
+    """A TaskForm body for one node of a torchrun job.  ``gpu_indices`` is a pinned device list
+    or a count; a count becomes ``HIP_VISIBLE_DEVICES=auto:N`` and the allocator picks the
+    devices (NUMA-packed, reservation-aware) when the job starts (``core/allocation.py``)."""
+    if isinstance(gpu_indices, int):
+        devices, n = f"auto:{gpu_indices}", gpu_indices
+    else:
+        devices, n = hip_visible_devices(gpu_indices), len(gpu_indices)
+    envs = [{"name": "HIP_VISIBLE_DEVICES", "value": devices}]
     envs += [{"name": k, "value": v} for k, v in RCCL_ENV.items()]
     params = [{"name": "--nnodes=", "value": str(nnodes)},
-              {"name": "--nproc_per_node=", "value": str(len(gpu_indices))},
+              {"name": "--nproc_per_node=", "value": str(n)},
               {"name": "--rdzv_backend=", "value": "c10d"},
               {"name": "--rdzv_endpoint=", "value": f"{master_host}:{master_port}"},
               {"name": "-m", "value": module}]

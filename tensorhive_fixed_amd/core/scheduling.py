@@ -10,6 +10,12 @@ A job is scheduled iff EVERY GPU of EVERY task (a task may own several GPUs thro
 ``HIP_VISIBLE_DEVICES=0,1,2,3``) is (a) not taken by an earlier job of this round and (b) free
 for at least ``schedule_queued_jobs_when_free_mins`` -- the owner's own upcoming reservations
 count as free.  All-or-nothing per job (gang semantics), first-fit in queue order.
+
+A task may also ask for a COUNT (``HIP_VISIBLE_DEVICES=auto:N``): the scheduler then picks N
+GPUs itself -- free long enough, allowed for the owner, not taken this round -- preferring the
+owner's own reservations and keeping the gang on as few NUMA nodes as possible
+(:func:`.allocation.pick`).  The reference could only run jobs whose tasks named their device.
+The choices are handed to ``business_execute``, which re-checks and claims them atomically.
 """
 from __future__ import annotations
 
@@ -32,16 +38,16 @@ def parse_device_list(value: str | None) -> list[int]:
 
 
 def task_gpu_indices(task) -> list[int]:
-    """GPU indices of a task: its HIP_VISIBLE_DEVICES env segment, else the legacy ``gpu_id``."""
-    for name, value in task.envs():
-        if name in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
-            idx = parse_device_list(value)
-            if idx:
-                return idx
-    m = _DEVICES_RE.match(task.command or "")
-    if m:
-        return parse_device_list(m.group(1))
-    return [] if task.gpu_id is None else [task.gpu_id]
+    """GPU indices of a task: the devices it holds right now (``gpu_allocations``), else its
+    pinned ``HIP_VISIBLE_DEVICES`` list; ``auto:N`` tasks that hold nothing yet have none."""
+    from .allocation import device_request, devices_of
+
+    tid = getattr(task, "id", None)
+    held = devices_of(tid) if tid is not None else []
+    if held:
+        return held
+    req = device_request(task)
+    return list(req.pinned) if req is not None and not req.auto else []
 
 
 def assigned_gpu_uuids(task, hardware_map: dict) -> list[str | None]:
@@ -67,6 +73,7 @@ class GreedyScheduler(Scheduler):
         upcoming reservation on the GPU (defaults to a DB lookup)."""
         self.free_window_mins = free_window_mins
         self._own = own_reservations or self._owner_has_upcoming_reservation
+        self.placements: dict[int, dict[int, list[str]]] = {}  # job id -> task id -> uuids (auto tasks)
 
     @staticmethod
     def _owner_has_upcoming_reservation(uuid: str, job, window: timedelta) -> bool:
@@ -74,28 +81,63 @@ class GreedyScheduler(Scheduler):
 
         return any(r.user_id == job.user_id for r in Reservation.upcoming_events_for_resource(uuid, window))
 
-    def schedule_jobs(self, jobs_to_hardware: dict, hardware_to_slots: dict) -> list:
+    def _usable(self, host, u, job, slots, window) -> tuple[bool, int]:
+        """(free long enough, preference tier) of one GPU for ``job``."""
+        slot = slots[host][u]
+        own = slot is not None and self._own(u, job, window)
+        if own:
+            return True, 0
+        if slot is None:
+            return True, 1
+        return slot >= self.free_window_mins, 2
+
+    def schedule_jobs(self, jobs_to_hardware: dict, hardware_to_slots: dict, gpu_info: dict | None = None) -> list:
+        """``gpu_info`` = ``{host: {uuid: {"index": i, "numa_node": n}}}`` for placing ``auto:N``
+        tasks (defaults: dict order, one NUMA node).  Chosen devices land in :attr:`placements`."""
+        from .allocation import Candidate, device_request, pick
+
         window = timedelta(minutes=self.free_window_mins)
         taken: set[tuple[str, str]] = set()
         scheduled = []
+        self.placements = {}
         for job in jobs_to_hardware:
             wanted: list[tuple[str, str]] = []
+            chosen: dict[int, list[str]] = {}
             ok = bool(job.tasks)
             for task in job.tasks:
+                host = task.hostname
+                slots = hardware_to_slots.get(host) or {}
+                eligible = (jobs_to_hardware.get(job) or {}).get(host)
+                req = device_request(task)
+                if req is not None and req.auto:
+                    info = (gpu_info or {}).get(host) or {}
+                    cands = []
+                    for pos, u in enumerate(slots):
+                        if (host, u) in taken or (host, u) in wanted or (eligible is not None and u not in eligible):
+                            continue
+                        usable, tier = self._usable(host, u, job, hardware_to_slots, window)
+                        if usable:
+                            g = info.get(u) or {}
+                            numa = g.get("numa_node")
+                            cands.append(Candidate(int(g.get("index", pos)), u,
+                                                   numa if isinstance(numa, int) and numa >= 0 else 0, tier))
+                    got = pick(cands, req.count)
+                    if got is None:
+                        ok = False
+                        break
+                    chosen[task.id] = [c.uuid for c in got]
+                    wanted += [(host, c.uuid) for c in got]
+                    continue
                 uuids = assigned_gpu_uuids(task, hardware_to_slots)
                 if not uuids or any(u is None for u in uuids):
                     ok = False  # a task must name GPUs that exist on its host
                     break
-                eligible = (jobs_to_hardware.get(job) or {}).get(task.hostname)
                 for u in uuids:
-                    key = (task.hostname, u)
+                    key = (host, u)
                     if key in taken or key in wanted or (eligible is not None and u not in eligible):
                         ok = False
                         break
-                    slot = hardware_to_slots[task.hostname][u]
-                    if slot is not None and self._own(u, job, window):
-                        slot = None
-                    if not (slot is None or slot >= self.free_window_mins):
+                    if not self._usable(host, u, job, hardware_to_slots, window)[0]:
                         ok = False
                         break
                     wanted.append(key)
@@ -104,4 +146,6 @@ class GreedyScheduler(Scheduler):
             if ok:
                 scheduled.append(job)
                 taken.update(wanted)
+                if chosen:
+                    self.placements[job.id] = chosen
         return scheduled

@@ -300,11 +300,13 @@ class JobSchedulingService(Service):
         return out
 
     def claimed(self, occ: dict) -> set[tuple[str, str]]:
-        """GPUs held by tasks we believe are running (monitoring may not show them yet)."""
+        """GPUs held by launching/running tasks (``gpu_allocations``; monitoring may not show
+        the processes yet), plus pinned running tasks from before allocations existed."""
         from ..models.orm import Task, TaskStatus
+        from .allocation import held_uuids
         from .scheduling import assigned_gpu_uuids
 
-        out = set()
+        out = held_uuids(self.d.infrastructure.snapshot().data)
         for t in Task.query.filter(Task._status == TaskStatus.running).all():
             for u in assigned_gpu_uuids(t, occ):
                 if u:
@@ -332,24 +334,42 @@ class JobSchedulingService(Service):
         return out
 
     def eligible(self, jobs) -> dict:
-        import copy
+        from ..controllers.nodes import filtered_view
 
         base = self.d.infrastructure.snapshot().data
         out = {}
         for job in jobs:
-            infra = job.user.filter_infrastructure_by_user_restrictions(copy.deepcopy(base)) if job.user else {}
+            infra = filtered_view(base, job.user.allowed_gpu_uuids()) if job.user else {}
             out[job] = {h: list(((e or {}).get("GPU") or {}).keys()) for h, e in infra.items()}
         return out
 
-    def _execute(self, job) -> bool:
+    def _execute(self, job, placements: dict | None = None) -> bool:
         from ..controllers.job import business_execute
 
-        content, status = business_execute(job.id)
+        content, status = business_execute(job.id, placements=placements, daemon=self.d)
         if status == 200:
             self.launch_log.append((job.id, time.time()))
             return True
         log.warning("scheduler could not execute job %s: %s", job.id, content.get("msg"))
         return False
+
+    def gpu_info(self) -> dict:
+        """{host: {uuid: {index, numa_node}}} for placing ``auto:N`` tasks."""
+        data = self.d.infrastructure.snapshot().data
+        return {h: {u: {"index": g.get("index"), "numa_node": g.get("numa_node")}
+                    for u, g in (((e or {}).get("GPU")) or {}).items()} for h, e in data.items()}
+
+    def refresh_allocations(self) -> None:
+        """Re-sync every task that holds devices (one ``th-run ls`` per host and user), so the
+        devices of finished tasks are released within one tick; then drop orphaned claims."""
+        from ..controllers import task as task_ctl
+        from ..models.orm import GpuAllocation
+        from . import allocation
+
+        cache = task_ctl.SessionCache()
+        for tid in sorted({a.task_id for a in GpuAllocation.query.all()}):
+            task_ctl.synchronize(tid, cache)
+        allocation.reap()
 
     def interferes_with_reservations(self, job, occ, period=timedelta(0)) -> bool:
         from ..models.orm import Reservation
@@ -366,6 +386,7 @@ class JobSchedulingService(Service):
         from sqlalchemy import and_, or_
 
         from ..models.orm import Job, JobStatus
+        from .allocation import device_request
         from .scheduling import assigned_gpu_uuids
 
         now = dates.utcnow()
@@ -380,6 +401,9 @@ class JobSchedulingService(Service):
             keys = set()
             ok = True
             for t in job.tasks:
+                req = device_request(t)
+                if req is None or req.auto:
+                    continue  # CPU-only, or placed (and checked) by business_execute's allocator
                 uu = assigned_gpu_uuids(t, occ)
                 if not uu or None in uu:
                     ok = False
@@ -404,8 +428,13 @@ class JobSchedulingService(Service):
         queue = Job.get_job_queue()
         if not queue:
             return
-        for job in self.scheduler.schedule_jobs(self.eligible(queue), self.gpu_slots(occ)):
-            self._execute(job)
+        sched = self.scheduler
+        try:
+            jobs = sched.schedule_jobs(self.eligible(queue), self.gpu_slots(occ), self.gpu_info())
+        except TypeError:  # a custom Scheduler with the reference's two-argument signature
+            jobs = sched.schedule_jobs(self.eligible(queue), self.gpu_slots(occ))
+        for job in jobs:
+            self._execute(job, (getattr(sched, "placements", None) or {}).get(job.id))
 
     def stop_with_grace(self, job_id: int):
         from ..controllers.job import business_stop
@@ -446,6 +475,7 @@ class JobSchedulingService(Service):
                 self.stop_with_grace(job.id)
 
     def do_run(self) -> None:
+        self.refresh_allocations()
         occ = self.occupancy()
         if not self.execute_scheduled(occ):
             self.execute_queued(occ)

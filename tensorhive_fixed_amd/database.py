@@ -32,6 +32,19 @@ def _fk_pragma(dbapi_conn, _record):
     cur.close()
 
 
+def _wal_pragma(dbapi_conn, _record):
+    """File databases run in WAL mode.  The daemon writes from API threads and service threads
+    at once; in the default rollback-journal mode a COMMIT must wait for every other
+    connection's SHARED lock, and a reader that then wants to write waits for the committer's
+    RESERVED lock -- a deadlock that only the 30 s busy timeout breaks (seen with concurrent
+    executes and scheduler ticks, tests/test_allocation.py).  In WAL mode readers never block a
+    commit.  WAL is a property of the database file; SQLite >= 3.7 (any TensorHive) opens it."""
+    cur = dbapi_conn.cursor()
+    cur.execute("PRAGMA journal_mode=WAL")
+    cur.execute("PRAGMA synchronous=NORMAL")
+    cur.close()
+
+
 def configure(uri: str | None = None):
     """(Re)create the engine for ``uri`` (default: the configured DB) and bind the session."""
     global _engine
@@ -48,6 +61,7 @@ def configure(uri: str | None = None):
             if uri.startswith("sqlite:///"):
                 Path(uri[len("sqlite:///"):]).expanduser().parent.mkdir(parents=True, exist_ok=True)
             eng = create_engine(uri, connect_args={"check_same_thread": False, "timeout": 30})
+            event.listen(eng, "connect", _wal_pragma)
         event.listen(eng, "connect", _fk_pragma)
         db_session.configure(bind=eng)
         _engine = eng
@@ -95,4 +109,18 @@ def ensure_db_with_current_schema() -> str:
         migrations.stamp(eng, migrations.HEAD)
         log.info("created a new database at revision %s", migrations.HEAD)
         return migrations.HEAD
-    return migrations.upgrade(eng)
+    rev = migrations.upgrade(eng)
+    create_daemon_tables(eng)
+    return rev
+
+
+DAEMON_TABLES = ("gpu_allocations",)
+
+
+def create_daemon_tables(eng=None) -> None:
+    """Tables the daemon owns outside the alembic revision chain (``gpu_allocations``): created
+    idempotently so an upgraded TensorHive database gains them without a new revision id (the
+    reference can still open it; it ignores tables it does not map)."""
+    import_models()
+    tables = [Base.metadata.tables[t] for t in DAEMON_TABLES if t in Base.metadata.tables]
+    Base.metadata.create_all(eng or engine(), tables=tables)

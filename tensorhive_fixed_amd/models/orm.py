@@ -23,7 +23,7 @@ import logging
 import re
 from datetime import timedelta
 
-from sqlalchemy import (Boolean, Column, DateTime, Enum, ForeignKey, Integer, String, Text, Time,
+from sqlalchemy import (Boolean, Column, DateTime, Enum, ForeignKey, Integer, String, Text, Time, UniqueConstraint,
                         and_, or_)
 from sqlalchemy.exc import MultipleResultsFound, NoResultFound
 from sqlalchemy.orm import relationship, validates
@@ -240,14 +240,22 @@ class User(CRUDModel, RestrictionAssignee, Base):
     def get_reservations(self, include_cancelled=False):
         return list(self.reservations) if include_cancelled else [r for r in self.reservations if not r.is_cancelled]
 
-    def filter_infrastructure_by_user_restrictions(self, infrastructure: dict) -> dict:
-        """Drop GPUs the user may not use, then hosts left without GPUs
-        (reference ``models/User.py:166-186``)."""
-        allowed = set()
+    def allowed_gpu_uuids(self) -> set[str] | None:
+        """GPUs the user's restrictions (own and group, unexpired) cover; ``None`` = all of them
+        (a global restriction)."""
+        allowed: set[str] = set()
         for r in self.get_restrictions(include_expired=False, include_group=True):
             if r.is_global:
-                return infrastructure
+                return None
             allowed.update(res.id for res in r.resources)
+        return allowed
+
+    def filter_infrastructure_by_user_restrictions(self, infrastructure: dict) -> dict:
+        """Drop GPUs the user may not use, then hosts left without GPUs, in place
+        (reference ``models/User.py:166-186``)."""
+        allowed = self.allowed_gpu_uuids()
+        if allowed is None:
+            return infrastructure
         for host in list(infrastructure):
             gpus = (infrastructure[host] or {}).get("GPU")
             if gpus is not None:
@@ -819,9 +827,14 @@ class Task(CRUDModel, Base):
 
     @property
     def full_command(self) -> str:
-        parts = [f"{n}={v}" for n, v in self.envs()]
+        return self.render(self.envs(), self.params())
+
+    def render(self, envs, params) -> str:
+        """``ENV=v ... command param value ...`` from explicit segment lists (the launch path
+        substitutes allocated devices before rendering, see ``core/allocation.py``)."""
+        parts = [f"{n}={v}" for n, v in envs]
         parts.append(self.command)
-        for n, v in self.params():
+        for n, v in params:
             if v == "":
                 parts.append(n)
             elif n.endswith("=") or n.endswith(" "):
@@ -870,6 +883,9 @@ class Task(CRUDModel, Base):
         d["cmdsegments"] = {"envs": envs, "params": params}
         d["fullCommand"] = self.full_command
         d["gpuId"] = self.gpu_id  # additive: first device of HIP_VISIBLE_DEVICES
+        # additive: the HIP indices this task holds while launching/running (auto:N requests
+        # resolve here; see core/allocation.py)
+        d["allocatedGpus"] = [a.gpu_index for a in GpuAllocation.for_task(self.id)] if self.id else []
         return d
 
 
@@ -989,3 +1005,39 @@ class Job(CRUDModel, Base):
     @staticmethod
     def get_jobs_running_from_queue():
         return Job.query.filter(Job.is_queued.is_(True)).filter(Job._status == JobStatus.running).all()
+
+
+# ----------------------------------------------------------------------------- allocations
+class GpuAllocation(CRUDModel, Base):
+    """One GPU held by one task while it is launching or running (daemon-owned, additive table).
+
+    The reference kept no record of which GPU a task held: the scheduler re-derived it from
+    ``CUDA_VISIBLE_DEVICES`` each tick and deduplicated within one round only
+    (``core/services/JobSchedulingService.py:140-168``).  Here every launch inserts one row per
+    device; the UNIQUE (hostname, gpu_index) constraint makes a double allocation impossible at
+    the database level, whatever thread or request tries it (see :mod:`..core.allocation`).
+    The table lives outside the alembic revision chain (created idempotently next to it), so a
+    database stays readable by TensorHive 1.1."""
+
+    __tablename__ = "gpu_allocations"
+    __table_args__ = (UniqueConstraint("hostname", "gpu_index", name="uq_gpu_allocations_host_gpu"),
+                      {"sqlite_autoincrement": True})
+    __public__ = ["id", "task_id", "job_id", "hostname", "gpu_index", "gpu_uuid", "created_at"]
+    id = Column(Integer, primary_key=True, autoincrement=True)
+    task_id = Column(Integer, ForeignKey("tasks.id", ondelete="CASCADE"), nullable=False, index=True)
+    job_id = Column(Integer, ForeignKey("jobs.id", ondelete="CASCADE"), nullable=True)
+    hostname = Column(String(40), nullable=False)
+    gpu_index = Column(Integer, nullable=False)
+    gpu_uuid = Column(String(64), nullable=True)
+    created_at = Column(DateTime, default=_utcnow, nullable=False)
+
+    def __repr__(self):
+        return f"<GpuAllocation task={self.task_id} {self.hostname}:{self.gpu_index}>"
+
+    @classmethod
+    def for_task(cls, task_id: int):
+        return cls.query.filter(cls.task_id == task_id).order_by(cls.id).all()
+
+    @classmethod
+    def held(cls) -> set[tuple[str, int]]:
+        return {(a.hostname, a.gpu_index) for a in cls.query.all()}

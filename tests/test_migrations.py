@@ -50,6 +50,13 @@ def test_upgrade_from_every_revision_matches_orm(tmp_path, orm_schema, rev):
     assert M.upgrade(eng) == M.HEAD
     with eng.connect() as c:
         assert M.current_revisions(c) == [M.HEAD]
+    # the revision chain builds exactly the reference schema; daemon-owned tables come on top,
+    # created next to it without a revision id (database.create_daemon_tables)
+    from tensorhive_fixed_amd.database import DAEMON_TABLES, create_daemon_tables
+
+    assert _schema(eng) == {t: c for t, c in orm_schema.items() if t not in DAEMON_TABLES}
+    create_daemon_tables(eng)
+    create_daemon_tables(eng)  # idempotent
     assert _schema(eng) == orm_schema
 
 

@@ -89,3 +89,47 @@ def test_three_tenants(daemon):
     daemon.infrastructure.publish("node-a", stub.sample("node-a"))
     sched.do_run()
     assert Job.get(jobs["bob-on-alice"].id).status is JobStatus.pending
+
+
+def test_three_tenants_unpinned_gang_jobs(daemon):
+    """The same node with jobs that ask for a COUNT of GPUs (``HIP_VISIBLE_DEVICES=auto:2``):
+    the scheduler picks pairs that respect every reservation, never overlaps them, and the
+    node fills up except where a reservation fences GPUs off."""
+    from tensorhive_fixed_amd.models.orm import GpuAllocation
+
+    stub = daemon.stub
+    alice, bob, carol = _user("alice"), _user("bob"), _user("carol")
+    g = Restriction(name="everyone", starts_at=UTC() - timedelta(days=1), is_global=True)
+    g.save()
+    for u in (alice, bob, carol):
+        g.apply_to_user(u)
+    uuid = [stub.gpu_uuid("node-a", i) for i in range(8)]
+    for u in uuid:
+        Resource(id=u, name="MI355X", hostname="node-a").save()
+    for user, gpus, start in ((alice, [0, 1], UTC() - timedelta(minutes=5)), (bob, [2, 3], UTC() - timedelta(minutes=5)),
+                              (carol, [4], UTC() + timedelta(minutes=10))):
+        for i in gpus:
+            Reservation(user_id=user.id, title=f"{user.username}-{i}", description="", resource_id=uuid[i],
+                        start=start, end=start + timedelta(hours=2)).save()
+    jobs = {n: _job(u, "auto:2", n) for n, u in (("a1", alice), ("b1", bob), ("c1", carol), ("b2", bob),
+                                                 ("a2", alice))}
+    sched = JobSchedulingService(3600.0, 5, 30)
+    daemon.add_service(sched)
+    sched.do_run()
+    got = {k: Job.get(j.id).tasks[0].as_dict()["allocatedGpus"] for k, j in jobs.items()}
+    status = {k: Job.get(j.id).status for k, j in jobs.items()}
+    assert got["a1"] == [0, 1]   # alice's own reservation first
+    assert got["b1"] == [2, 3]   # bob's own reservation first
+    assert got["c1"] in ([4, 5], [4, 6], [4, 7])  # carol's upcoming GPU 4 is hers to use
+    assert status["b2"] is JobStatus.running and status["a2"] is JobStatus.pending
+    flat = [i for v in got.values() for i in v]
+    assert len(flat) == len(set(flat)) == 8  # no GPU twice, node full
+    assert 4 not in got["b2"]  # carol's upcoming reservation is fenced off for bob
+    held = {i for _h, i in GpuAllocation.held()}
+    assert held == set(range(8))
+    # a1 finishes -> its pair goes back to alice's queue entry a2 on the next tick
+    node = daemon.transports.get("node-a")
+    node.exit_task(Job.get(jobs["a1"].id).tasks[0].pid)
+    daemon.infrastructure.publish("node-a", stub.sample("node-a"))
+    sched.do_run()
+    assert Job.get(jobs["a2"].id).tasks[0].as_dict()["allocatedGpus"] == [0, 1]

@@ -77,10 +77,20 @@ def test_spawn_log_and_exit(local):
     assert len(tail) == 1
 
 
+def _log_or_empty(local, user, name):
+    try:
+        return local.fetch_log("localhost", user, name)[0]
+    except FileNotFoundError:
+        return []
+
+
 def test_interrupt_foreground_task(local):
     me = getpass.getuser()
-    pid = local.spawn("sleep 300; echo not reached", "localhost", me, name_appendix="int")
+    pid = local.spawn("echo started; sleep 300; echo not reached", "localhost", me, name_appendix="int")
     assert _wait(lambda: _alive(pid))
+    # interrupt once the command runs: a SIGINT that lands while `bash -l` still sources profile
+    # scripts can be swallowed by one of their children, and bash then goes on to `sleep 300`
+    assert _wait(lambda: "started" in _log_or_empty(local, me, "int"))
     assert local.terminate(pid, "localhost", me, gracefully=True) == 0
     assert _wait(lambda: not _alive(pid), 15)
     lines, _ = local.fetch_log("localhost", me, "int")

@@ -113,8 +113,20 @@ def test_poll_latency_benchmark():
     from tensorhive_fixed_amd import benchmarks
 
     out = benchmarks.poll_latency(requests=30, nodes=2, gpus=8, warmup=2)
-    res = out["results"]["/api/nodes/metrics"]
-    assert res["requests"] == 30 and 0 < res["p50_ms"] <= res["p99_ms"]
+    for mode in ("admin_inprocess", "user_inprocess", "user_socket"):
+        res = out["results"][mode]["/api/nodes/metrics"]
+        assert res["requests"] == 30 and 0 < res["p50_ms"] <= res["p99_ms"]
+    assert out["user_visible_gpus"] == 8  # the restricted user sees half of 2 x 8 GPUs
+
+
+def test_multitenant_benchmark_small():
+    from tensorhive_fixed_amd import benchmarks
+
+    out = benchmarks.multitenant(jobs_per_user=3, duration_s=(0.2, 0.4), arrival_s=0.05)
+    assert out["jobs"] == out["completed"] == 9
+    assert out["queue_wait_p50_ms"] <= out["queue_wait_p99_ms"]
+    assert 0 < out["node_gpu_util"] <= 1
+    assert out["violations"] == {"mallory": ["bob"]} and out["walled_ttys"] == ["pts/7"]
 
 
 def test_doctor_reports_without_gpu(monkeypatch):
