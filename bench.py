@@ -27,6 +27,27 @@ sys.path.insert(0, ROOT)
 BASELINE_TOKENS_PER_SEC = None  # the reference publishes no throughput
 
 
+def daemon_poll_latency() -> dict | None:
+    """The other half of the north-star metric (BASELINE.json): p50/p99 of ``GET /api/nodes/metrics``
+    for a non-admin user with per-GPU restrictions, over HTTP to the daemon's threaded server
+    (8 simulated nodes x 8 GPUs).  Runs in a child process AFTER the timed training steps, so it
+    cannot touch the measured region; any failure reports null instead of failing the bench."""
+    import subprocess
+
+    code = ("import json; from tensorhive_fixed_amd import benchmarks as b; "
+            "r = b.poll_latency(500); print(json.dumps({k: v['/api/nodes/metrics'] for k, v in r['results'].items()}))")
+    try:
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+        res = json.loads(out.stdout.strip().splitlines()[-1])
+        return {"poll_p50_ms_user_socket": res["user_socket"]["p50_ms"],
+                "poll_p99_ms_user_socket": res["user_socket"]["p99_ms"],
+                "poll_p50_ms_user_inprocess": res["user_inprocess"]["p50_ms"],
+                "poll_p50_ms_admin_inprocess": res["admin_inprocess"]["p50_ms"],
+                "setup": "8 simulated nodes x 8 GPUs, non-admin with per-GPU restrictions, HTTP keep-alive"}
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)[:200]}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -40,9 +61,10 @@ def main() -> int:
     ap.add_argument("--bucket-mb", type=float, default=float(os.environ.get("TH_BENCH_BUCKET_MB", "256")))
     ap.add_argument("--grad-accum", type=int, default=int(os.environ.get("TH_BENCH_ACCUM", "1")))
     ap.add_argument("--zero", type=int, default=None, help="1 = sharded optimizer (default for N > 1), 0 = replicated")
+    ap.add_argument("--daemon-bench", type=int, default=1,
+                    help="rank 0 also measures the daemon's dashboard poll latency after the timed steps")
     args = ap.parse_args()
 
-    os.environ.setdefault("PYTORCH_ALLOC_CONF", "expandable_segments:True")  # no fragmentation near the HBM limit
     import torch
 
     from tensorhive_fixed_amd.models.llama3 import LlamaConfig
@@ -94,6 +116,7 @@ def main() -> int:
         "final_loss": round(res["loss"], 4),
     }
     if info.is_main:
+        line["daemon"] = daemon_poll_latency() if args.daemon_bench else None
         print(json.dumps(line), flush=True)
     shutdown()
     return 0

@@ -1,4 +1,4 @@
-"""Known-byte HBM load for counter calibration: ``python scripts/hbm_stream.py SECONDS KIND``.
+"""Known-byte HBM load for counter calibration: ``python scripts/hbm_stream.py SECONDS KIND [half]``.
 
 KIND ``add`` runs ``y += x`` over 1 GiB fp32 tensors (a shader kernel: 2 reads + 1 write per
 element), ``copy`` runs ``y.copy_(x)`` (the runtime's blit kernel).  Prints one JSON line with
@@ -14,6 +14,7 @@ import torch
 def main():
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 3.0
     kind = sys.argv[2] if len(sys.argv) > 2 else "add"
+    half = len(sys.argv) > 3 and sys.argv[3] == "half"  # idle as long as each burst ran: ~half the rate
     n = 1 << 28  # 1 GiB of fp32
     x = torch.ones(n, device="cuda", dtype=torch.float32)
     y = torch.zeros_like(x)
@@ -22,6 +23,7 @@ def main():
     t0 = time.perf_counter()
     done = 0
     while time.perf_counter() - t0 < secs:
+        tb = time.perf_counter()
         for _ in range(8):
             if kind == "add":
                 y.add_(x)
@@ -29,6 +31,8 @@ def main():
                 y.copy_(x)
         torch.cuda.synchronize()
         done += 8
+        if half:
+            time.sleep(time.perf_counter() - tb)
     dt = time.perf_counter() - t0
     print(json.dumps({"kind": kind, "iters": done, "bytes": done * per, "seconds": round(dt, 3),
                       "GBps": round(done * per / dt / 1e9, 1)}), flush=True)

@@ -7,9 +7,13 @@ RoPE theta = 5e5, RMSNorm eps = 1e-5, untied LM head.
 
 Per block the data flow is chosen for MI355X:
   x -> RMSNorm (HIP) -> ONE fused QKV GEMM [4096 -> 6144] -> RoPE in place + causal GQA flash
-  attention straight out of the packed qkv buffer (HIP, MFMA) -> O-proj GEMM with the residual
-  add fused into the GEMM (addmm beta = 1) -> RMSNorm (HIP) -> ONE fused gate|up GEMM
-  [4096 -> 28672] -> SwiGLU (HIP) -> down GEMM with fused residual add.
+  attention straight out of the packed qkv buffer (HIP, MFMA) -> O-proj GEMM -> residual add
+  fused INTO the next RMSNorm (``rmsnorm_add_fork``: one kernel reads the projection and the
+  residual stream, writes their bf16 sum and the normalised row) -> ONE fused gate|up GEMM
+  [4096 -> 28672] -> SwiGLU (HIP) -> down GEMM, whose residual add is again taken by the next
+  block's (or the final) RMSNorm.  ``TH_ADD_NORM=0`` selects the older flow, where the O-proj and
+  down GEMMs add the residual in an ``addmm`` beta = 1 epilogue; both flows are checked against
+  each other in ``tests/test_rmsnorm_add.py``.
 The LM head is fused with the cross-entropy (chunked, logits never materialised whole).
 Every weight gradient is written by its producing GEMM/kernel into the flat DDP buffer.
 """

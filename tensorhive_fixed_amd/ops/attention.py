@@ -26,14 +26,20 @@ from .rope import rope_inplace
 
 
 def attention_backend() -> str:
-    """``TH_ATTN_BACKEND`` if set, else ``hip`` when the flash kernel is in libthk.so."""
+    """``TH_ATTN_BACKEND`` if set, else ``hip``.  On a GPU the flash kernel must be in
+    libthk.so: a missing or stale library raises instead of falling back to SDPA (a silent
+    fallback would measure torch's attention and report it as ours).  Without a GPU the answer
+    is ``hip`` too -- CPU tensors take the fp32 reference path inside :func:`qkv_attention`."""
     env = os.environ.get("TH_ATTN_BACKEND")
     if env:
         return env
-    try:
-        return "hip" if hasattr(_lib.load(), "th_flash_attn_fwd") else "sdpa"
-    except (RuntimeError, OSError):
-        return "sdpa"
+    if not torch.cuda.is_available():
+        return "hip"
+    lib = _lib.load()  # raises with the build hint when libthk.so is missing
+    if not hasattr(lib, "th_flash_attn_fwd"):
+        raise RuntimeError("libthk.so has no th_flash_attn_fwd: rebuild it (python -m tensorhive_fixed_amd.ops.build) "
+                           "or select TH_ATTN_BACKEND=sdpa explicitly")
+    return "hip"
 
 
 def attention_reference(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True) -> torch.Tensor:

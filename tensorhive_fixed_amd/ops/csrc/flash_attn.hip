@@ -845,6 +845,10 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
     if (total > 0) {
       load_ld(0, 0);
       write_ld(0);
+      // the first wait_dma_barrier() waits on vmcnt only: retire these LDS writes before it, so
+      // other waves' iteration-0 reads of lse/delta are ordered by that barrier (in the loop the
+      // mid-iteration lgkmcnt(0) + s_barrier does this for later tiles)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       dma_tile(0, 0, 0);
       adv(lh, lt);
       if (total > 1) load_ld(lh, lt);

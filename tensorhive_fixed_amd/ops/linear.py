@@ -1,9 +1,10 @@
 """Linear layers whose weight gradient lands directly in the flat DDP gradient buffer.
 
-GEMMs are plain library GEMMs (hipBLASLt through ``torch.mm``/``addmm``); what is custom is the
-data flow: the residual add of the attention-out and MLP-down projections is fused into the
-GEMM epilogue (``addmm`` with beta = 1), and ``dW = dYᵀ·X`` is written by the GEMM itself into
-``weight.main_grad`` (see ``_grad.deliver``).
+GEMMs are hipBLASLt (``torch.mm``/``addmm``) or the gfx950 TN kernel for weight gradients; what is
+custom is the data flow: ``dW = dYᵀ·X`` is written by the GEMM itself into ``weight.main_grad``
+(see ``_grad.deliver``).  By default the residual adds of the attention-out and MLP-down
+projections are NOT done here but in the next RMSNorm (``rmsnorm_add_fork``, ``models/llama3.py``);
+with ``TH_ADD_NORM=0`` they run as an ``addmm`` beta = 1 epilogue of these GEMMs (``residual=``).
 
 Operand layouts (measured, ``scripts/gemm_layouts.py`` -> ``profiles/r01_gemm/``): hipBLASLt on
 gfx950 is fastest when both operands are contiguous along the reduction dim.  The forward

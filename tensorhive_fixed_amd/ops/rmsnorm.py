@@ -47,7 +47,8 @@ def _fwd_add(y: torch.Tensor, r: torch.Tensor, w: torch.Tensor, eps: float):
         r2 = r2.contiguous()
     T = y2.shape[0]
     if y2.is_cuda:
-        if y2.dtype != torch.bfloat16 or r2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or D % 8:
+        if (y2.dtype != torch.bfloat16 or r2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or D % 8
+                or w.numel() != D or r2.shape != y2.shape):
             raise ValueError("rmsnorm_add kernel needs bf16 [T, D] inputs, bf16 [D] weight, D % 8 == 0")
         xsum = torch.empty_like(y2)
         h = torch.empty_like(y2)

@@ -89,3 +89,37 @@ def test_flash_fwd_variants_match_reference(variant):
     o, _ = flash_fwd(qkv, B, S, Hq, Hkv, D, variant=variant)
     ref = _ref(qkv.float(), B, S, Hq, Hkv, D)
     assert (o.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("S,Hq,Hkv", [(4096, 32, 8), (8192, 8, 2)], ids=["S4096_bench_heads", "S8192_model_max"])
+def test_flash_long_sequences_match_fp32(S, Hq, Hkv):
+    """The training shapes: S = 4096 (the bench) with Llama-3-8B's 32/8 heads, and S = 8192 (the
+    model's maximum) -- fp32 reference computed per head group in chunks to bound its memory."""
+    from tensorhive_fixed_amd.ops.attention import _split, flash_bwd, flash_fwd
+    torch.manual_seed(3)
+    B, D = 1, 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
+    do = torch.randn_like(o)
+    dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)
+    rep = Hq // Hkv
+    mask = torch.ones(S, S, dtype=torch.bool, device="cuda").triu(1)
+    for kv in range(Hkv):  # one GQA group at a time: q heads kv*rep..(kv+1)*rep share k/v head kv
+        x = qkv.float().requires_grad_(True)
+        q, k, v = _split(x, B, S, Hq, Hkv, D)
+        qg = q[:, :, kv * rep:(kv + 1) * rep].transpose(1, 2)  # [B, rep, S, D]
+        kg, vg = k[:, :, kv:kv + 1].transpose(1, 2), v[:, :, kv:kv + 1].transpose(1, 2)
+        s = (qg @ kg.transpose(-1, -2)) / math.sqrt(D)
+        p = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
+        og = (p @ vg).transpose(1, 2).reshape(B * S, rep * D)
+        sl = slice(kv * rep * D, (kv + 1) * rep * D)
+        rel_o = ((o[:, sl].float() - og).norm() / og.norm()).item()
+        assert rel_o < 1e-2, f"group {kv} fwd rel err {rel_o}"
+        og.backward(do[:, sl].float())
+        g = x.grad
+        for name, cols in (("dq", sl), ("dk", slice((Hq + kv) * D, (Hq + kv + 1) * D)),
+                           ("dv", slice((Hq + Hkv + kv) * D, (Hq + Hkv + kv + 1) * D))):
+            ref = g[:, cols]
+            rel = ((dqkv[:, cols].float() - ref).norm() / (ref.norm() + 1e-6)).item()
+            assert rel < 2e-2, f"group {kv} {name} rel err {rel}"
+        del x, q, k, v, s, p, og, g

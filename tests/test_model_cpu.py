@@ -87,3 +87,25 @@ def test_gate_up_swiglu_cpu_matches_unfused():
     swiglu(linear(h2, w2)).backward(g)
     assert torch.allclose(h.grad.float(), h2.grad.float(), atol=3e-2, rtol=2e-2)
     assert torch.allclose(w.grad.float(), w2.grad.float(), atol=3e-2, rtol=2e-2)
+
+
+def test_add_norm_flow_matches_addmm_epilogue_flow_cpu(monkeypatch):
+    """The default flow (residual adds fused into the next RMSNorm) and the TH_ADD_NORM=0 flow
+    (residual added in the GEMM epilogue) give the same loss and gradients within bf16 noise."""
+    from tensorhive_fixed_amd.models import llama3
+
+    cfg = LlamaConfig.tiny()
+    tok = torch.randint(0, cfg.vocab_size, (2, 48), generator=torch.Generator().manual_seed(1))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 48), generator=torch.Generator().manual_seed(2))
+    out = {}
+    for flag in (True, False):
+        monkeypatch.setattr(llama3, "ADD_NORM", flag)
+        model = Llama(cfg, device="cpu", dtype=torch.bfloat16, seed=5)
+        loss = model(tok, tgt)
+        loss.backward()
+        out[flag] = (float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+    assert abs(out[True][0] - out[False][0]) < 1e-2
+    for n, a in out[True][1].items():
+        b = out[False][1][n]
+        rel = float((a - b).norm() / (b.norm() + 1e-8))
+        assert rel < 3e-2, (n, rel)
