@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 
 GPU_METRICS = ["fan_speed", "mem_free", "mem_used", "mem_total", "utilization", "mem_util", "temp", "power",
                # new (MI355X telemetry)
-               "hotspot_temp", "mem_temp", "gfx_clock", "mem_clock", "hbm_bw", "mfma_busy", "xgmi_read",
+               "hotspot_temp", "mem_temp", "gfx_clock", "mem_clock", "hbm_bw", "mfma_busy", "hbm_contention", "xgmi_read",
                "xgmi_write", "energy"]
 CPU_METRICS = ["mem_free", "mem_used", "mem_total", "utilization"]
 
@@ -60,8 +60,10 @@ SCHEMAS: dict[str, dict] = {
     "UserLoginForm": {"required": ["username", "password"],
                       "properties": {"username": "string", "password": "string"}},
     "TaskForm": {"required": ["command", "hostname"],
-                 "properties": {"jobId": "integer", "command": "string", "hostname": "string", "cmdsegments": "object"}},
-    "TaskUpdateForm": {"required": [], "properties": {"command": "string", "hostname": "string", "cmdsegments": "object"}},
+                 "properties": {"jobId": "integer", "command": "string", "hostname": "string", "cmdsegments": "object",
+                                "maxRestarts": "integer"}},
+    "TaskUpdateForm": {"required": [], "properties": {"command": "string", "hostname": "string", "cmdsegments": "object",
+                                                    "maxRestarts": "integer"}},
     # new: multi-task launch generator (torchrun / torch TCP ranks / TF2 TF_CONFIG / TF1 ClusterSpec)
     "TaskGenerateForm": {"required": ["template", "placements"],
                          "properties": {"template": "string", "command": "string", "module": "string",
@@ -204,6 +206,8 @@ EXTRA_OPERATIONS: list[Op] = [
        body="TaskGenerateForm", body_name="form", tag="jobs"),
     Op("PUT", "/jobs/{id}/reservation/{reservation_id}", "job.attach_to_reservation", "jwt",      # new
        [P("id"), P("reservation_id"), Q("siblings", "boolean")], tag="jobs"),
+    Op("GET", "/tasks/{id}/training", "task.get_training_metrics", "jwt",                       # new
+       ID + [Q("lines", "integer")], tag="tasks"),
 ]
 
 COMPAT_OPERATION_COUNT = 66

@@ -240,6 +240,7 @@ class LauncherConfig:
     rdzv_backend: str
     master_port: int
     bucket_mb: int
+    restart_delay: float = 5.0  # seconds between a failed run and its restart (task maxRestarts)
 
 
 @dataclass
@@ -400,6 +401,7 @@ def load_config(directory: Path | str | None = None) -> Config:
             rdzv_backend=main.str("launcher", "rdzv_backend", "c10d"),
             master_port=main.int("launcher", "master_port", 29500),
             bucket_mb=main.int("launcher", "bucket_mb", 256),
+            restart_delay=main.float("launcher", "restart_delay", 5.0),
         ),
     )
 

@@ -178,11 +178,11 @@ def business_execute(id: int, placements: dict | None = None, daemon=None):
                 continue
             devices = [i for i, _u in plan.get(t.id, [])]
             cmd = allocation.render_command(t, devices)
-            todo.append((t, (cmd, t.hostname, job.user.username, str(t.id))))
+            todo.append((t, (cmd, t.hostname, job.user.username, str(t.id), t.max_restarts)))
 
-        def spawn(cmd, host, user, tid):
+        def spawn(cmd, host, user, tid, max_restarts):
             try:
-                return task_nursery.spawn(cmd, host, user, name_appendix=tid)
+                return task_nursery.spawn(cmd, host, user, name_appendix=tid, max_restarts=max_restarts)
             except Exception as e:  # noqa: BLE001
                 log.warning("spawn of task %s failed: %s", tid, e)
                 return None

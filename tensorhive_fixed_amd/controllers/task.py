@@ -14,6 +14,7 @@ not interpreted (north star: no CUDA paths).
 from __future__ import annotations
 
 import logging
+import re
 import time
 
 from sqlalchemy.exc import NoResultFound
@@ -28,19 +29,19 @@ log = logging.getLogger(__name__)
 
 
 class SessionCache:
-    """(host, user) -> set of live task pids, fetched lazily once.  The monotonic time each list
+    """(host, user) -> live task sessions keyed by pid (current and spawn-time), fetched lazily once.  The monotonic time each list
     was fetched is kept: a launch that finished after it is not judged by that list."""
 
     def __init__(self):
-        self._d: dict[tuple[str, str], set[int] | Exception] = {}
+        self._d: dict[tuple[str, str], dict[int, dict] | Exception] = {}
         self.fetched_at: dict[tuple[str, str], float] = {}
 
-    def pids(self, host: str, user: str) -> set[int]:
+    def pids(self, host: str, user: str) -> dict[int, dict]:
         key = (host, user)
         if key not in self._d:
             self.fetched_at[key] = time.monotonic()
             try:
-                self._d[key] = set(task_nursery.running_pids(host, user))
+                self._d[key] = task_nursery.running_sessions(host, user)
             except Exception as e:  # noqa: BLE001
                 self._d[key] = e
         v = self._d[key]
@@ -88,9 +89,19 @@ def synchronize(task_id: int, cache: SessionCache | None = None) -> None:
             task.pid = None
             task.save()
             allocation.release_task(task.id)  # the task's devices are free again
-        elif task.status is not TaskStatus.running:
-            task.status = TaskStatus.running  # re-adopt a live session after a daemon restart
-            task.save()
+        else:
+            sess = live[task.pid]
+            if isinstance(sess, dict):  # the restart policy may have replaced the process
+                cur = int(sess.get("pid") or task.pid)
+                if cur != task.pid:
+                    task.pid = cur
+                    task.save()
+                if sess.get("restarts") not in (None, ""):
+                    lec = sess.get("last_exit_code")
+                    task.record_restarts(int(sess["restarts"]), int(lec) if lec not in (None, "") else None)
+            if task.status is not TaskStatus.running:
+                task.status = TaskStatus.running  # re-adopt a live session after a daemon restart
+                task.save()
 
 
 def parse_gpu_id_from_command(value: str | None) -> int | None:
@@ -166,6 +177,12 @@ def get_log(id: int, tail: bool = False):
     return business_get_log(id, tail)
 
 
+@guarded(not_found="task.not_found")
+def get_training_metrics(id: int, lines: int = 400):
+    _owned_task(id)
+    return business_get_training_metrics(id, lines)
+
+
 # ------------------------------------------------------------------- business functions
 def business_get_all(job_id: int | None, sync_all: bool | None):
     if job_id is not None:
@@ -191,6 +208,8 @@ def business_create(task: dict, job_id: int):
     job = Job.get(job_id)
     t.save()
     _apply_segments(t, task.get("cmdsegments") or {})
+    if task.get("maxRestarts") is not None:
+        t.set_max_restarts(task["maxRestarts"])
     t.save()
     job.add_task(t)
     return {"msg": M("task.create.success"), "task": t.as_dict()}, 201
@@ -217,6 +236,8 @@ def business_update(id: int, newValues: dict):
                 t.segment_links.remove(lk)
             t.save()
             _apply_segments(t, value or {})
+        elif key == "maxRestarts":
+            t.set_max_restarts(value)
     t.save()
     return {"msg": M("task.update.success"), "task": t.as_dict()}, 201
 
@@ -244,7 +265,8 @@ def business_spawn(id: int, cache: SessionCache | None = None):
     assert t.hostname, "hostname is empty"
     assert job is not None and job.user is not None, "user does not exist"
     try:
-        pid = task_nursery.spawn(t.full_command, t.hostname, job.user.username, name_appendix=str(t.id))
+        pid = task_nursery.spawn(t.full_command, t.hostname, job.user.username, name_appendix=str(t.id),
+                                 max_restarts=t.max_restarts)
     except (task_nursery.SpawnError, ConnectionError, KeyError, AssertionError) as e:
         return {"msg": M("task.spawn.failure.backend", reason=e)}, 500
     t.pid = pid
@@ -266,6 +288,42 @@ def business_terminate(id: int, gracefully: bool | None = True, cache: SessionCa
     if code != 0:
         return {"msg": M("task.terminate.failure.exit_code"), "exit_code": code}, 202
     return {"msg": M("task.terminate.success"), "exit_code": code}, 200
+
+
+_TRAIN_LINE = re.compile(r"\[th-train\] step=(\d+) loss=([-+0-9.eEnainf]+) tokens/s=([0-9.]+)(?: world=(\d+))?")
+
+
+def parse_training_lines(lines) -> list[dict]:
+    """``[th-train] step=S loss=L tokens/s=T world=W`` lines of the Llama payload
+    (``workloads/llama3_ddp.py``) -> [{step, loss, tokensPerSec, world}] in log order."""
+    out = []
+    for line in lines:
+        m = _TRAIN_LINE.search(line)
+        if m:
+            out.append({"step": int(m.group(1)), "loss": float(m.group(2)), "tokensPerSec": float(m.group(3)),
+                        "world": int(m.group(4)) if m.group(4) else None})
+    return out
+
+
+@guarded(not_found="task.not_found", assertion="task.get_log.failure.assertions")
+def business_get_training_metrics(id: int, lines: int = 400):
+    """Training progress read from the task's log tail: the series of ``[th-train]`` lines and
+    the latest tokens/s, which the dashboard charts next to the task (SURVEY §5 metrics row)."""
+    t = Task.get(id)
+    job = t.job
+    assert t.hostname, "hostname is empty"
+    assert job is not None and job.user is not None, "user does not exist"
+    try:
+        out, path = task_nursery.fetch_log(t.hostname, job.user.username, t.id, tail=True,
+                                           tail_lines=max(1, min(int(lines), 5000)))
+    except FileNotFoundError as e:
+        return {"msg": M("task.get_log.failure.not_found", location=e)}, 404
+    except ConnectionError as e:
+        return {"msg": M("task.get_log.failure.assertions", reason=e)}, 500
+    series = parse_training_lines(out)
+    last = series[-1] if series else None
+    return {"msg": M("task.get_log.success"), "path": path, "series": series, "last": last,
+            "tokensPerSec": last["tokensPerSec"] if last else None}, 200
 
 
 @guarded(not_found="task.not_found", assertion="task.get_log.failure.assertions")

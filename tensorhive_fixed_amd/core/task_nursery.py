@@ -7,6 +7,8 @@ Public functions keep the reference's shape:
   * :func:`terminate` -- ``gracefully=True`` SIGINT, ``None`` SIGTERM (was ``screen -X quit``),
     ``False`` SIGKILL, always to the whole process group (torchrun + every rank);
   * :func:`running` -- live sessions of a user on a host, ONE round trip per host (``th-run ls``);
+  * restart policy: ``max_restarts`` > 0 makes ``th-run`` start a failed run again (new pid, same
+    log and session name); :func:`running_sessions` maps the spawn-time pid to the current one;
   * :func:`fetch_log` -- ``~/TensorHiveLogs/task_<id>.log`` (whole file or tail).
 Names (``tensorhive_task_<id>``) and log paths are unchanged.  Every task gets
 ``TENSORHIVE_TASK_ID=<id>`` in its environment, which the telemetry uses to attribute GPU
@@ -75,21 +77,27 @@ def _run(host: str, user: str, cmd: str, timeout: float | None = None) -> Result
     return _client(host, user).run(host, cmd, timeout=timeout)
 
 
-def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | None = None) -> str:
+def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | None = None,
+                        max_restarts: int = 0) -> str:
     name = session_name(task_id)
     logf = log_path(task_id)
     env = {"TENSORHIVE_TASK_ID": str(task_id), **(extra_env or {})}
     env_args = " ".join(f"--env {shlex.quote(f'{k}={v}')}" for k, v in env.items())
     th = shlex.quote(th_run)
-    primary = (f"{th} spawn --name {name} --log {logf} {env_args} -- bash -lc {shlex.quote(command)}")
+    policy = ""
+    if max_restarts and int(max_restarts) > 0:  # th-run restarts a failed run (the fallback cannot)
+        policy = f" --max-restarts {int(max_restarts)} --restart-delay {get_config().launcher.restart_delay:g}"
+    primary = (f"{th} spawn --name {name} --log {logf} {env_args}{policy} -- bash -lc {shlex.quote(command)}")
     envs = " ".join(f"{k}={shlex.quote(str(v))}" for k, v in env.items())
     fallback = (f"mkdir -p $(dirname {logf}) && ( {envs} setsid bash -lc {shlex.quote(command)} "
                 f"> >(tee -a {logf} >/dev/null) 2>&1 < /dev/null & echo $! )")
     return f"if command -v {th} >/dev/null 2>&1 || [ -x {th} ]; then {primary}; else {fallback}; fi"
 
 
-def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra_env: dict | None = None) -> int:
-    r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), extra_env))
+def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra_env: dict | None = None,
+          max_restarts: int = 0) -> int:
+    r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), extra_env,
+                                                 max_restarts))
     if r.exception is not None:
         raise SpawnError(f"connection failed: {r.exception}")
     try:
@@ -132,6 +140,17 @@ def running(hostname: str, user: str) -> list[dict]:
 
 def running_pids(hostname: str, user: str) -> list[int]:
     return [int(d["pid"]) for d in running(hostname, user)]
+
+
+def running_sessions(hostname: str, user: str) -> dict[int, dict]:
+    """Live sessions keyed by every pid a task is known by: its current pid and, for a session
+    the restart policy has restarted, the pid it was spawned with (what the daemon stored)."""
+    out: dict[int, dict] = {}
+    for d in running(hostname, user):
+        out[int(d["pid"])] = d
+        if d.get("first_pid") not in (None, ""):
+            out.setdefault(int(d["first_pid"]), d)
+    return out
 
 
 def fetch_log(hostname: str, user: str, task_id, tail: bool = False, tail_lines: int = 10) -> tuple[list[str], str]:

@@ -6,7 +6,8 @@ call.  Backends:
 
 * :class:`AmdSmiBackend` -- the local node through ``native/lib/libthsmi.so`` (C++, amdsmi +
   /proc + KFD sysfs), optionally augmented by the gfx950 probe kernel (``mfma_busy``,
-  ``hbm_bw``) from ``libthk.so``.
+  ``hbm_contention``) from ``libthk.so``; ``hbm_bw`` (GB/s) comes from libthsmi's calibrated
+  ``mem_activity_acc`` rate.
 * :class:`RemoteBackend` -- other nodes: ``th-smi`` over the node transport, either one-shot or
   as a persistent ``th-smi --stream MS`` over one multiplexed SSH channel (sub-second cadence
   without a round trip per poll).
@@ -121,7 +122,7 @@ class AmdSmiBackend(TelemetryBackend):
 
 class GpuProbe:
     """Runs the gfx950 th-probe kernel (libthk.so) at a low duty cycle and derives
-    ``mfma_busy`` / ``hbm_bw`` per device from the slowdown against the best (idle) sample."""
+    ``mfma_busy`` / ``hbm_contention`` per device from the slowdown against the best (idle) sample."""
 
     def __init__(self, period: float = 1.0, device: int = 0, n_wg: int = 8, mfma_iters: int = 512):
         from ..ops import _lib
@@ -129,11 +130,13 @@ class GpuProbe:
         self.lib = _lib.load()
         self.lib.th_probe_init.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         self.lib.th_probe_sample.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        self.lib.th_probe_last_latency_us.restype = ctypes.c_double
         rc = self.lib.th_probe_init(device, n_wg, 1024)
         if rc != 0:
             raise RuntimeError(f"th_probe_init failed ({rc})")
         self.period, self.device, self.n_wg, self.iters = period, device, n_wg, mfma_iters
         self.best_mfma = math.inf
+        self.best_lat = math.inf
         self.best_bw = 0.0
         self._last = 0.0
         self._cached: dict | None = None
@@ -143,8 +146,9 @@ class GpuProbe:
         n = self.lib.th_probe_sample(self.n_wg, self.iters, out)
         if n <= 0:
             raise RuntimeError(f"th_probe_sample failed ({n})")
+        lat = float(self.lib.th_probe_last_latency_us())
         return [{"xcc": int(out[5 * i]), "mfma_us": out[5 * i + 1], "hbm_us": out[5 * i + 2],
-                 "hbm_GBps": out[5 * i + 3]} for i in range(n)]
+                 "hbm_GBps": out[5 * i + 3], "latency_us": lat} for i in range(n)]
 
     def maybe_sample(self) -> dict | None:
         now = time.time()
@@ -154,11 +158,18 @@ class GpuProbe:
         rows = self.sample_raw()
         mfma = sum(r["mfma_us"] for r in rows) / len(rows)
         bw = sum(r["hbm_GBps"] for r in rows)
+        lat = rows[0]["latency_us"]
         self.best_mfma = min(self.best_mfma, mfma)
+        self.best_lat = min(self.best_lat, lat) if lat > 0 else self.best_lat
         self.best_bw = max(self.best_bw, bw)
-        busy = max(0.0, 1.0 - self.best_mfma / mfma) * 100 if mfma > 0 else None
+        # Two ways a tenant shows up: it shares SIMDs with the probe (the MFMA chain slows down), or it
+        # holds every CU's register file (the probe waits for a CU; the in-kernel time is unchanged).
+        # mfma_busy is the larger of the two slowdowns.
+        busy_chain = max(0.0, 1.0 - self.best_mfma / mfma) if mfma > 0 else 0.0
+        busy_wait = max(0.0, 1.0 - self.best_lat / lat) if lat > 0 and math.isfinite(self.best_lat) else 0.0
+        busy = max(busy_chain, busy_wait) * 100 if mfma > 0 else None
         share = max(0.0, 1.0 - bw / self.best_bw) * 100 if self.best_bw > 0 else None
-        self._cached = {self.device: {"mfma_busy": _metric(busy, "%"), "hbm_bw": _metric(share, "%"),
+        self._cached = {self.device: {"mfma_busy": _metric(busy, "%"), "hbm_contention": _metric(share, "%"),
                                       "probe_xcds": _metric(len({r["xcc"] for r in rows}), "")}}
         return self._cached
 
@@ -269,6 +280,7 @@ class StubBackend(TelemetryBackend):
                         "gfx_clock": _metric(2400 if busy else 150, "MHz"), "mem_clock": _metric(2000, "MHz"),
                         "xgmi_read": _metric(0.0, "GB/s"), "xgmi_write": _metric(0.0, "GB/s"),
                         "energy": _metric(180 + util * 8, "W"),  # accumulator-derived power, as libthsmi
+                        "hbm_bw": _metric(round(util * 0.6 * 102.0, 1), "GB/s"),  # umc % x calibrated GB/s
                     },
                     "processes": procs,
                 }

@@ -167,7 +167,8 @@ class SimulatedNode(FakeTransport):
     GPUs named by ``HIP_VISIBLE_DEVICES`` with their owner and ``TENSORHIVE_TASK_ID``, exactly as
     the amdsmi backend would report them.  ``exit_task(pid)`` simulates a task finishing."""
 
-    _SPAWN = re.compile(r"spawn --name (\S+) --log (\S+)((?: --env \S+)*) -- bash -lc (.*?); else")
+    _SPAWN = re.compile(r"spawn --name (\S+) --log (\S+)((?: --env \S+)*)(?: --max-restarts (\d+) --restart-delay \S+)?"
+                        r" -- bash -lc (.*?); else")
     _SIG = re.compile(r"then \S+ (interrupt|terminate|kill) --pid (\d+)")
 
     def __init__(self, host: str, telemetry=None, first_pid: int = 40000):
@@ -197,8 +198,8 @@ class SimulatedNode(FakeTransport):
             return self._signal(int(m.group(2)), m.group(1), user)
         if re.search(r"then \S+ ls; fi", command):
             with self._lock:
-                lines = [json.dumps({k: v for k, v in s.items() if k != "gpus"}) for s in self.sessions.values()
-                         if s["user"] == user]
+                lines = [json.dumps({k: v for k, v in s.items() if k not in ("gpus", "env")})
+                         for s in self.sessions.values() if s["user"] == user]
             return Result(self.host, "\n".join(lines) + ("\n" if lines else ""), "", 0)
         m = re.match(r"(?:tail -n (\d+)|cat) (\S+)$", command.strip())
         if m:
@@ -234,7 +235,8 @@ class SimulatedNode(FakeTransport):
                     self.telemetry.processes[k] = [p for p in procs if p["pid"] != pid]
 
     def _spawn(self, m, user) -> Result:
-        name, logf, envs, cmd = m.group(1), m.group(2), m.group(3), m.group(4)
+        name, logf, envs, cmd = m.group(1), m.group(2), m.group(3), m.group(5)
+        max_restarts = int(m.group(4) or 0)
         env = dict(shlex.split(e)[0].split("=", 1) for e in re.findall(r"--env (\S+)", envs))
         cmd = shlex.split(cmd)[0] if cmd.startswith("'") else cmd
         gpus = []
@@ -245,12 +247,38 @@ class SimulatedNode(FakeTransport):
             pid = self._next
             self._next += 1
             self.sessions[pid] = {"name": name, "pid": pid, "pgid": pid, "started": time.time(), "user": user,
-                                  "command": cmd, "log": logf, "gpus": gpus}
+                                  "command": cmd, "log": logf, "gpus": gpus, "first_pid": pid, "restarts": 0,
+                                  "max_restarts": max_restarts, "env": env}
             self.logs[logf] = [f"[simulated] {cmd}"]
         if self.telemetry is not None:
             for g in gpus:
                 self.telemetry.add_process(self.host, g, pid, user or "", cmd[:80], env.get("TENSORHIVE_TASK_ID"))
         return Result(self.host, f"{pid}\n", "", 0)
+
+    def crash_task(self, pid: int, code: int = 1) -> int | None:
+        """Simulate a run exiting with ``code``: like th-run, a session with restarts left is
+        started again under a new pid (returned); otherwise it ends (None)."""
+        with self._lock:
+            s = self.sessions.get(pid)
+        if s is None:
+            return None
+        if s["restarts"] >= s["max_restarts"]:
+            self.exit_task(pid, f"[simulated] exit code {code}")
+            return None
+        self._drop_gpu_process(pid)
+        with self._lock:
+            self.sessions.pop(pid, None)
+            new = self._next
+            self._next += 1
+            s = dict(s, pid=new, pgid=new, restarts=s["restarts"] + 1, last_exit_code=code)
+            self.sessions[new] = s
+            self.logs.setdefault(s["log"], []).append(
+                f"[th-run] exit code {code}; restart {s['restarts']}/{s['max_restarts']}")
+        if self.telemetry is not None:
+            for g in s["gpus"]:
+                self.telemetry.add_process(self.host, g, new, s["user"] or "", s["command"][:80],
+                                           s["env"].get("TENSORHIVE_TASK_ID"))
+        return new
 
     def exit_task(self, pid: int, line: str = "[simulated] done") -> None:
         with self._lock:
@@ -262,7 +290,8 @@ class SimulatedNode(FakeTransport):
 
     def _signal(self, pid: int, verb: str, user) -> Result:
         with self._lock:
-            s = self.sessions.get(pid)
+            s = self.sessions.get(pid) or next((x for x in self.sessions.values() if x.get("first_pid") == pid), None)
+            pid = s["pid"] if s else pid
         if s is None or (user and s["user"] != user):
             return Result(self.host, "", f"no such session {pid}", 1)
         self.exit_task(pid, f"[simulated] {verb}")

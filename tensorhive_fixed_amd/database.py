@@ -114,11 +114,12 @@ def ensure_db_with_current_schema() -> str:
     return rev
 
 
-DAEMON_TABLES = ("gpu_allocations",)
+DAEMON_TABLES = ("gpu_allocations", "task_restart_policies")
 
 
 def create_daemon_tables(eng=None) -> None:
-    """Tables the daemon owns outside the alembic revision chain (``gpu_allocations``): created
+    """Tables the daemon owns outside the alembic revision chain (``gpu_allocations``,
+    ``task_restart_policies``): created
     idempotently so an upgraded TensorHive database gains them without a new revision id (the
     reference can still open it; it ignores tables it does not map)."""
     import_models()

@@ -886,7 +886,31 @@ class Task(CRUDModel, Base):
         # additive: the HIP indices this task holds while launching/running (auto:N requests
         # resolve here; see core/allocation.py)
         d["allocatedGpus"] = [a.gpu_index for a in GpuAllocation.for_task(self.id)] if self.id else []
+        pol = TaskRestartPolicy.for_task(self.id) if self.id else None
+        d["maxRestarts"] = pol.max_restarts if pol else 0  # additive: restart policy (th-run)
+        d["restarts"] = pol.restarts if pol else 0
         return d
+
+    @property
+    def max_restarts(self) -> int:
+        pol = TaskRestartPolicy.for_task(self.id) if self.id else None
+        return pol.max_restarts if pol else 0
+
+    def set_max_restarts(self, n: int) -> None:
+        assert isinstance(n, int) and not isinstance(n, bool) and 0 <= n <= 100, \
+            "maxRestarts must be an integer in [0, 100]"
+        pol = TaskRestartPolicy.for_task(self.id)
+        if pol is None:
+            pol = TaskRestartPolicy(task_id=self.id, max_restarts=n, restarts=0)
+        pol.max_restarts = n
+        pol.save()
+
+    def record_restarts(self, restarts: int, last_exit_code=None) -> None:
+        pol = TaskRestartPolicy.for_task(self.id)
+        if pol is not None and (pol.restarts != restarts or pol.last_exit_code != last_exit_code):
+            pol.restarts = restarts
+            pol.last_exit_code = last_exit_code
+            pol.save()
 
 
 class Job(CRUDModel, Base):
@@ -1041,3 +1065,23 @@ class GpuAllocation(CRUDModel, Base):
     @classmethod
     def held(cls) -> set[tuple[str, int]]:
         return {(a.hostname, a.gpu_index) for a in cls.query.all()}
+
+
+class TaskRestartPolicy(CRUDModel, Base):
+    """Restart policy of one task (daemon-owned, additive table, like ``gpu_allocations``).
+
+    The reference only detects a failed task (``core/services/JobSchedulingService.py:210-252``);
+    here ``max_restarts`` is passed to ``th-run spawn --max-restarts`` and the supervisor starts a
+    run that exited non-zero again, unless the stop was requested.  ``restarts`` and
+    ``last_exit_code`` mirror the supervisor's session state at each synchronisation."""
+
+    __tablename__ = "task_restart_policies"
+    __public__ = ["task_id", "max_restarts", "restarts", "last_exit_code"]
+    task_id = Column(Integer, ForeignKey("tasks.id", ondelete="CASCADE"), primary_key=True)
+    max_restarts = Column(Integer, default=0, nullable=False)
+    restarts = Column(Integer, default=0, nullable=False)
+    last_exit_code = Column(Integer, nullable=True)
+
+    @classmethod
+    def for_task(cls, task_id: int):
+        return cls.query.filter(cls.task_id == task_id).first()

@@ -4,11 +4,15 @@
 //   screen -Dm -S tensorhive_task_<id> bash -c "<cmd> |& tee --ignore-interrupts <log>" & echo $!
 // and controlled with `screen -X stuff ^C` / `screen -X quit` / `kill -9` / `screen -ls`.
 //
-//   th-run spawn --name NAME --log FILE [--state-dir DIR] [--env K=V]... [--cwd DIR] -- CMD ARGS...
+//   th-run spawn --name NAME --log FILE [--state-dir DIR] [--env K=V]... [--cwd DIR]
+//                [--max-restarts N] [--restart-delay S] -- CMD ARGS...
 //       Detaches (double fork + setsid), starts CMD in its OWN process group with stdout+stderr
 //       on a pipe, and prints the pid of CMD (== its pgid) on stdout, then returns.  A small
 //       monitor process (own session, ignores SIGINT/SIGTERM/SIGHUP like `tee --ignore-interrupts`)
-//       copies the pipe into FILE line by line, reaps CMD and records its exit status.
+//       copies the pipe into FILE line by line, reaps CMD and records its exit status.  With
+//       --max-restarts N a run that exits non-zero is started again (new pid/pgid, same log,
+//       TH_RUN_RESTART=k in its env) up to N times, unless the stop was requested through th-run
+//       (SURVEY §5 failure row: restart policy; the reference only detects failures).
 //   th-run interrupt|terminate|kill (--name NAME | --pid PID) [--state-dir DIR]
 //       SIGINT / SIGTERM / SIGKILL to the task's whole process group (torchrun + all ranks).
 //   th-run ls [--all] [--state-dir DIR]     one JSON object per session (live ones by default)
@@ -59,6 +63,8 @@ std::string dirname_of(const std::string& p) {
   size_t k = p.rfind('/');
   return k == std::string::npos ? "." : (k == 0 ? "/" : p.substr(0, k));
 }
+
+std::string stop_marker(const std::string& dir, const std::string& name) { return dir + "/" + name + ".stop"; }
 
 std::string expand_home(const std::string& p) {
   if (!p.empty() && p[0] == '~') {
@@ -125,6 +131,13 @@ bool pid_alive(long pid) {
   return errno == EPERM;
 }
 
+// Live = the task runs, or it is between a failed run and its restart (monitor alive).
+bool session_alive(KV& kv) {
+  if (kv["status"] == "running") return pid_alive(atol(kv["pid"].c_str()));
+  if (kv["status"] == "restarting") return pid_alive(atol(kv["monitor_pid"].c_str()));
+  return false;
+}
+
 std::string to_json(const KV& kv, bool alive) {
   std::string o = "{";
   bool first = true;
@@ -132,7 +145,9 @@ std::string to_json(const KV& kv, bool alive) {
     if (!first) o += ",";
     first = false;
     const bool num = it.first == "pid" || it.first == "pgid" || it.first == "monitor_pid" ||
-                     it.first == "exit_code" || it.first == "started" || it.first == "ended";
+                     it.first == "exit_code" || it.first == "started" || it.first == "ended" ||
+                     it.first == "first_pid" || it.first == "restarts" || it.first == "max_restarts" ||
+                     it.first == "last_exit_code";
     o += "\"" + json_escape(it.first) + "\":";
     if (num && !it.second.empty())
       o += it.second;
@@ -157,7 +172,8 @@ void write_all(int fd, const char* p, ssize_t n) {
 
 int usage() {
   fprintf(stderr,
-          "usage: th-run spawn --name NAME --log FILE [--state-dir D] [--env K=V].. [--cwd D] -- CMD..\n"
+          "usage: th-run spawn --name NAME --log FILE [--state-dir D] [--env K=V].. [--cwd D]\n"
+          "                    [--max-restarts N] [--restart-delay S] -- CMD..\n"
           "       th-run interrupt|terminate|kill (--name NAME | --pid PID) [--state-dir D]\n"
           "       th-run ls [--all] [--state-dir D] | status --name NAME | wait --name NAME [--timeout S]\n");
   return 2;
@@ -166,7 +182,8 @@ int usage() {
 struct Args {
   std::string cmd, name, log, state_dir, cwd;
   long pid = -1;
-  double timeout = -1;
+  double timeout = -1, restart_delay = 1.0;
+  int max_restarts = 0;
   bool all = false;
   std::vector<std::string> env;
   std::vector<std::string> argv;
@@ -206,6 +223,14 @@ bool parse(int argc, char** argv, Args& a) {
       std::string t;
       if (!need(t)) return false;
       a.timeout = atof(t.c_str());
+    } else if (s == "--max-restarts") {
+      std::string t;
+      if (!need(t)) return false;
+      a.max_restarts = atoi(t.c_str());
+    } else if (s == "--restart-delay") {
+      std::string t;
+      if (!need(t)) return false;
+      a.restart_delay = atof(t.c_str());
     } else if (s == "--all") {
       a.all = true;
     } else {
@@ -248,92 +273,123 @@ int do_spawn(Args& a) {
   pid_t p2 = fork();
   if (p2 < 0) _exit(1);
   if (p2 > 0) _exit(0);
-  // monitor process.  INT/TERM/HUP stay BLOCKED across the fork below: the task child resets them
-  // to SIG_DFL before unblocking (a signal sent the moment its pid is known is then delivered with
-  // the default action instead of being lost to an inherited SIG_IGN); the monitor ignores them.
+  // monitor process.  INT/TERM/HUP are BLOCKED across every fork below: the task child resets
+  // them to SIG_DFL before unblocking (a signal sent the moment its pid is known is then delivered
+  // with the default action instead of being lost to an inherited SIG_IGN); the monitor ignores them.
   sigset_t guard, prev;
   sigemptyset(&guard);
   sigaddset(&guard, SIGINT);
   sigaddset(&guard, SIGTERM);
   sigaddset(&guard, SIGHUP);
-  sigprocmask(SIG_BLOCK, &guard, &prev);
   signal(SIGPIPE, SIG_IGN);
-  int out[2];
-  if (pipe(out) != 0) _exit(1);
   int logfd = open(a.log.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
   if (logfd < 0) _exit(1);
-  pid_t c = fork();
-  if (c < 0) _exit(1);
-  if (c == 0) {  // the task: own process group, default signal dispositions
-    setpgid(0, 0);
-    signal(SIGINT, SIG_DFL);
-    signal(SIGTERM, SIG_DFL);
-    signal(SIGHUP, SIG_DFL);
-    signal(SIGPIPE, SIG_DFL);
-    sigprocmask(SIG_SETMASK, &prev, nullptr);
-    dup2(out[1], 1);
-    dup2(out[1], 2);
-    close(out[0]);
-    close(out[1]);
-    close(logfd);
-    close(hs[1]);
-    int devnull = open("/dev/null", O_RDONLY);
-    if (devnull >= 0) {
-      dup2(devnull, 0);
-      close(devnull);
-    }
-    for (const auto& e : a.env) putenv(strdup(e.c_str()));
-    if (!a.cwd.empty() && chdir(expand_home(a.cwd).c_str()) != 0) perror("th-run: chdir");
-    std::vector<char*> av;
-    for (auto& s : a.argv) av.push_back(const_cast<char*>(s.c_str()));
-    av.push_back(nullptr);
-    execvp(av[0], av.data());
-    fprintf(stderr, "th-run: exec %s: %s\n", av[0], strerror(errno));
-    _exit(127);
-  }
-  setpgid(c, c);  // race-free: both sides set it
-  signal(SIGINT, SIG_IGN);
-  signal(SIGTERM, SIG_IGN);
-  signal(SIGHUP, SIG_IGN);
-  sigprocmask(SIG_SETMASK, &prev, nullptr);
-  close(out[1]);
+  const std::string stopf = stop_marker(a.state_dir, a.name);
+  unlink(stopf.c_str());  // a fresh session: no stop request yet
   KV st;
   st["name"] = a.name;
-  st["pid"] = std::to_string((long)c);
-  st["pgid"] = std::to_string((long)c);
   st["monitor_pid"] = std::to_string((long)getpid());
   st["started"] = std::to_string((long)time(nullptr));
   st["log"] = a.log;
   std::string cmdline;
   for (auto& s : a.argv) cmdline += (cmdline.empty() ? "" : " ") + s;
   st["cmd"] = cmdline;
-  st["status"] = "running";
-  write_state(a.state_dir, a.name, st);
-  long cpid = (long)c;
-  write_all(hs[1], (const char*)&cpid, sizeof cpid);
-  close(hs[1]);
-  int devnull = open("/dev/null", O_RDWR);
-  if (devnull >= 0) {
-    dup2(devnull, 0);
-    dup2(devnull, 1);
-    dup2(devnull, 2);
-    close(devnull);
-  }
-  char buf[65536];
+  st["max_restarts"] = std::to_string(a.max_restarts);
+  int restarts = 0, code = -1;
   for (;;) {
-    ssize_t n = read(out[0], buf, sizeof buf);
-    if (n < 0 && errno == EINTR) continue;
-    if (n <= 0) break;
-    write_all(logfd, buf, n);
+    sigprocmask(SIG_BLOCK, &guard, &prev);
+    int out[2];
+    if (pipe(out) != 0) _exit(1);
+    pid_t c = fork();
+    if (c < 0) _exit(1);
+    if (c == 0) {  // the task: own process group, default signal dispositions
+      setpgid(0, 0);
+      signal(SIGINT, SIG_DFL);
+      signal(SIGTERM, SIG_DFL);
+      signal(SIGHUP, SIG_DFL);
+      signal(SIGPIPE, SIG_DFL);
+      sigprocmask(SIG_SETMASK, &prev, nullptr);
+      dup2(out[1], 1);
+      dup2(out[1], 2);
+      close(out[0]);
+      close(out[1]);
+      close(logfd);
+      if (restarts == 0) close(hs[1]);
+      int devnull = open("/dev/null", O_RDONLY);
+      if (devnull >= 0) {
+        dup2(devnull, 0);
+        close(devnull);
+      }
+      for (const auto& e : a.env) putenv(strdup(e.c_str()));
+      putenv(strdup(("TH_RUN_RESTART=" + std::to_string(restarts)).c_str()));
+      if (!a.cwd.empty() && chdir(expand_home(a.cwd).c_str()) != 0) perror("th-run: chdir");
+      std::vector<char*> av;
+      for (auto& s : a.argv) av.push_back(const_cast<char*>(s.c_str()));
+      av.push_back(nullptr);
+      execvp(av[0], av.data());
+      fprintf(stderr, "th-run: exec %s: %s\n", av[0], strerror(errno));
+      _exit(127);
+    }
+    setpgid(c, c);  // race-free: both sides set it
+    signal(SIGINT, SIG_IGN);
+    signal(SIGTERM, SIG_IGN);
+    signal(SIGHUP, SIG_IGN);
+    sigprocmask(SIG_SETMASK, &prev, nullptr);
+    close(out[1]);
+    st["pid"] = std::to_string((long)c);
+    st["pgid"] = std::to_string((long)c);
+    if (restarts == 0) st["first_pid"] = std::to_string((long)c);
+    st["restarts"] = std::to_string(restarts);
+    st["status"] = "running";
+    write_state(a.state_dir, a.name, st);
+    if (restarts == 0) {
+      long cpid = (long)c;
+      write_all(hs[1], (const char*)&cpid, sizeof cpid);
+      close(hs[1]);
+      int devnull = open("/dev/null", O_RDWR);
+      if (devnull >= 0) {
+        dup2(devnull, 0);
+        dup2(devnull, 1);
+        dup2(devnull, 2);
+        close(devnull);
+      }
+    }
+    char buf[65536];
+    for (;;) {
+      ssize_t n = read(out[0], buf, sizeof buf);
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) break;
+      write_all(logfd, buf, n);
+    }
+    close(out[0]);
+    int wst = 0;
+    while (waitpid(c, &wst, 0) < 0 && errno == EINTR) {
+    }
+    code = WIFEXITED(wst) ? WEXITSTATUS(wst) : (WIFSIGNALED(wst) ? 128 + WTERMSIG(wst) : -1);
+    // Restart policy: a failed run is restarted up to --max-restarts times, unless the exit was
+    // requested (interrupt/terminate/kill through th-run leave a stop marker first).
+    if (code == 0 || restarts >= a.max_restarts || access(stopf.c_str(), F_OK) == 0) break;
+    ++restarts;
+    char note[256];
+    const int k = snprintf(note, sizeof note, "[th-run] exit code %d; restart %d/%d in %.1f s\n", code, restarts,
+                           a.max_restarts, a.restart_delay);
+    write_all(logfd, note, k);
+    st["status"] = "restarting";
+    st["last_exit_code"] = std::to_string(code);
+    write_state(a.state_dir, a.name, st);
+    bool stop = false;
+    for (double w = 0; w < a.restart_delay && !stop; w += 0.05) {
+      usleep(50000);
+      stop = access(stopf.c_str(), F_OK) == 0;
+    }
+    if (stop) break;
   }
-  int wst = 0;
-  while (waitpid(c, &wst, 0) < 0 && errno == EINTR) {
-  }
-  int code = WIFEXITED(wst) ? WEXITSTATUS(wst) : (WIFSIGNALED(wst) ? 128 + WTERMSIG(wst) : -1);
   st["status"] = "exited";
   st["exit_code"] = std::to_string(code);
+  st["restarts"] = std::to_string(restarts);
   st["ended"] = std::to_string((long)time(nullptr));
   write_state(a.state_dir, a.name, st);
+  unlink(stopf.c_str());
   close(logfd);
   _exit(0);
 }
@@ -343,8 +399,27 @@ bool lookup(const Args& a, KV& kv) {
   return read_state(a.state_dir + "/" + a.name + ".state", kv);
 }
 
+// Name of the session whose current or first pid is `pid` ("" if none).
+std::string session_of_pid(const std::string& dir, long pid) {
+  DIR* d = opendir(dir.c_str());
+  if (!d) return "";
+  std::string found;
+  struct dirent* e;
+  while ((e = readdir(d)) != nullptr && found.empty()) {
+    std::string n = e->d_name;
+    if (n.size() < 7 || n.substr(n.size() - 6) != ".state") continue;
+    KV kv;
+    if (read_state(dir + "/" + n, kv) && kv["status"] != "exited" &&
+        (atol(kv["pgid"].c_str()) == pid || atol(kv["first_pid"].c_str()) == pid))
+      found = kv["name"];
+  }
+  closedir(d);
+  return found;
+}
+
 int do_signal(const Args& a, int sig) {
   long pg = a.pid;
+  std::string name = a.name;
   if (pg <= 0) {
     KV kv;
     if (!lookup(a, kv)) {
@@ -353,6 +428,16 @@ int do_signal(const Args& a, int sig) {
     }
     if (kv["status"] == "exited") return 4;
     pg = atol(kv["pgid"].c_str());
+  } else {
+    name = session_of_pid(a.state_dir, pg);
+    if (!name.empty()) {  // signal the current incarnation of a restarted task
+      KV kv;
+      if (read_state(a.state_dir + "/" + name + ".state", kv)) pg = atol(kv["pgid"].c_str());
+    }
+  }
+  if (!name.empty()) {  // a requested stop is never undone by the restart policy
+    FILE* f = fopen(stop_marker(a.state_dir, name).c_str(), "w");
+    if (f) fclose(f);
   }
   if (pg <= 0) return 3;
   if (kill(-(pid_t)pg, sig) != 0 && kill((pid_t)pg, sig) != 0) {
@@ -371,7 +456,7 @@ int do_ls(const Args& a) {
     if (n.size() < 7 || n.substr(n.size() - 6) != ".state") continue;
     KV kv;
     if (!read_state(a.state_dir + "/" + n, kv)) continue;
-    const bool alive = kv["status"] == "running" && pid_alive(atol(kv["pid"].c_str()));
+    const bool alive = session_alive(kv);
     if (!alive && !a.all) continue;
     printf("%s\n", to_json(kv, alive).c_str());
   }
@@ -382,8 +467,7 @@ int do_ls(const Args& a) {
 int do_status(const Args& a) {
   KV kv;
   if (!lookup(a, kv)) return 3;
-  const bool alive = kv["status"] == "running" && pid_alive(atol(kv["pid"].c_str()));
-  printf("%s\n", to_json(kv, alive).c_str());
+  printf("%s\n", to_json(kv, session_alive(kv)).c_str());
   return 0;
 }
 

@@ -45,7 +45,22 @@ struct Gpu {
   // previous accumulators for rates
   uint64_t xr_prev = 0, xw_prev = 0, energy_prev = 0;
   uint64_t ts_prev = 0;
+  // HBM bandwidth from gpu_metrics.mem_activity_acc, rate taken over >= 1 s windows (the firmware
+  // table refreshes in steps; a 0.25 s delta is too coarse).
+  uint64_t mem_acc_prev = 0, mem_ts_prev = 0;
+  double hbm_gbps = -1;
 };
+
+// GB/s per unit/s of mem_activity_acc on MI355X, fitted against timed device streams (add 5.78 TB/s,
+// copy 5.01 TB/s, half-duty add 2.89 TB/s: 0.0938 / 0.0973 / 0.0945; profiles/r02_telemetry/
+// hbm_calibration.jsonl).  Override with TENSORHIVE_HBM_GBPS_PER_ACC.
+double hbm_gbps_per_acc() {
+  static double k = [] {
+    const char* e = getenv("TENSORHIVE_HBM_GBPS_PER_ACC");
+    return (e && *e) ? atof(e) : 0.0952;
+  }();
+  return k;
+}
 
 std::mutex g_mu;
 bool g_init = false;
@@ -335,6 +350,15 @@ std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd,
       if (xw >= g.xw_prev) xw_rate = (xw - g.xw_prev) * 1024.0 / dt / 1e9;
       if (gm.energy_accumulator >= g.energy_prev) e_rate = (gm.energy_accumulator - g.energy_prev) * 15.259e-6 / dt;
     }
+    const uint64_t macc = gm.mem_activity_acc;
+    if (g.mem_ts_prev == 0 || macc < g.mem_acc_prev) {
+      g.mem_acc_prev = macc;
+      g.mem_ts_prev = ts;
+    } else if (ts - g.mem_ts_prev >= 1000000000ull) {
+      g.hbm_gbps = (macc - g.mem_acc_prev) / ((ts - g.mem_ts_prev) * 1e-9) * hbm_gbps_per_acc();
+      g.mem_acc_prev = macc;
+      g.mem_ts_prev = ts;
+    }
     g.xr_prev = xr;
     g.xw_prev = xw;
     g.energy_prev = gm.energy_accumulator;
@@ -356,6 +380,7 @@ std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd,
   m += ",\"xgmi_read\":" + metric("GB/s", xr_rate >= 0, xr_rate);
   m += ",\"xgmi_write\":" + metric("GB/s", xw_rate >= 0, xw_rate);
   m += ",\"energy\":" + metric("W", e_rate >= 0, e_rate);
+  m += ",\"hbm_bw\":" + metric("GB/s", g.hbm_gbps >= 0, g.hbm_gbps);
   m += "}";
 
   std::map<long, uint64_t> host;  // amdsmi / KFD: host pid -> vram bytes

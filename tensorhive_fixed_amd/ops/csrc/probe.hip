@@ -74,6 +74,8 @@ struct ProbeState {
   float4v* hbm = nullptr;
   float* sink = nullptr;
   unsigned long long* host = nullptr;  // pinned, device-mapped
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_latency_us = 0.f;  // launch-to-completion of the last probe, incl. waiting for a free CU
   int max_wg = 0;
   long per_wg_vec = 0;
 };
@@ -91,6 +93,7 @@ extern "C" int th_probe_init(int device, int max_wg, int slice_kb) {
   hipMemsetAsync(g_probe.hbm, 0, (size_t)max_wg * g_probe.per_wg_vec * 16, g_probe.stream);
   if (hipMalloc((void**)&g_probe.sink, 64) != hipSuccess) return 4;
   if (hipHostMalloc((void**)&g_probe.host, (size_t)max_wg * 4 * 8, hipHostMallocMapped) != hipSuccess) return 5;
+  if (hipEventCreate(&g_probe.ev0) != hipSuccess || hipEventCreate(&g_probe.ev1) != hipSuccess) return 6;
   hipStreamSynchronize(g_probe.stream);
   g_probe.device = device;
   return 0;
@@ -101,10 +104,14 @@ extern "C" int th_probe_sample(int n_wg, int mfma_iters, double* out) {
   if (g_probe.device < 0 || n_wg <= 0 || n_wg > g_probe.max_wg) return -1;
   unsigned long long* dev_host = nullptr;
   if (hipHostGetDevicePointer((void**)&dev_host, g_probe.host, 0) != hipSuccess) return 2;
+  hipEventRecord(g_probe.ev0, g_probe.stream);
   th_probe_kernel<<<n_wg, 256, 0, g_probe.stream>>>(g_probe.hbm, g_probe.per_wg_vec, mfma_iters, dev_host,
                                                     g_probe.sink);
   if (hipGetLastError() != hipSuccess) return 3;
+  hipEventRecord(g_probe.ev1, g_probe.stream);
   if (hipStreamSynchronize(g_probe.stream) != hipSuccess) return 4;
+  float ms = 0.f;
+  g_probe.last_latency_us = hipEventElapsedTime(&ms, g_probe.ev0, g_probe.ev1) == hipSuccess ? ms * 1e3f : 0.f;
   for (int i = 0; i < n_wg; ++i) {
     const unsigned long long* r = g_probe.host + 4 * i;
     const double mfma_us = r[1] / 100.0, hbm_us = r[2] / 100.0;  // 100 MHz ticks
@@ -117,8 +124,15 @@ extern "C" int th_probe_sample(int n_wg, int mfma_iters, double* out) {
   return n_wg;
 }
 
+// Queue-to-completion time of the last probe (us).  A tenant kernel that holds every CU's register
+// file (e.g. a 1-wave/SIMD MFMA GEMM) never shares a SIMD with the probe, so it does not slow the
+// probe's MFMA chain; it delays the probe's dispatch instead -- this latency is what rises.
+extern "C" double th_probe_last_latency_us(void) { return (double)g_probe.last_latency_us; }
+
 extern "C" int th_probe_shutdown(void) {
   if (g_probe.device < 0) return 0;
+  hipEventDestroy(g_probe.ev0);
+  hipEventDestroy(g_probe.ev1);
   hipFree(g_probe.hbm);
   hipFree(g_probe.sink);
   hipHostFree(g_probe.host);

@@ -3,8 +3,9 @@
 Launched one process per GPU (``torchrun --nproc_per_node N -m
 tensorhive_fixed_amd.workloads.llama3_ddp``), typically by the tensorhive job queue through the
 ``torchrun`` task template with ``HIP_VISIBLE_DEVICES`` taken from the reservation.  It prints
-``[th-train] step=… tokens/s=…`` lines which the daemon's log parser turns into the tokens/s
-reported on the dashboard and in BASELINE.md.
+``[th-train] step=… tokens/s=…`` lines; the daemon parses them from the task log tail
+(``GET /api/tasks/{id}/training``, ``controllers/task.py:parse_training_lines``) and the dashboard
+charts the series on the task's page.
 
 One step = forward + backward (gradient buckets all-reduced -- or, with the ZeRO-1 sharded
 optimizer that is the default for world > 1, reduce-scattered -- over RCCL while backward runs) +
