@@ -25,7 +25,7 @@ from .. import __version__
 from ..config import get_config
 from ..database import db_session
 from . import auth
-from .spec import EXTRA_OPERATIONS, OPERATIONS, SCHEMAS, Op, openapi_document
+from .spec import EXTRA_OPERATIONS, OPERATIONS, RESPONSES, SCHEMAS, Op, SchemaError, openapi_document, validate
 
 log = logging.getLogger(__name__)
 _EXT = "tensorhive_fixed_amd"
@@ -100,33 +100,19 @@ def _query_args(op: Op) -> dict:
     return out
 
 
-_PY_TYPES = {"string": (str,), "integer": (int,), "number": (int, float), "boolean": (bool,), "array": (list,),
-             "object": (dict,)}
-
-
 def _validate_body(schema_name: str):
+    """The JSON body against its spec schema, nested objects included (``cmdsegments`` entries,
+    ``scheduleDays`` names, date-time strings, bounds): a violation is a 400 problem, as
+    connexion's validator answered, before any controller runs."""
     body = request.get_json(silent=True)
     if body is None:
         raise ValidationError("Request body is not valid JSON" if request.data else "Request body is required")
     if not isinstance(body, dict):
         raise ValidationError(f"{body!r} is not of type 'object'")
-    sch = SCHEMAS[schema_name]
-    for f in sch["required"]:
-        if f not in body:
-            raise ValidationError(f"'{f}' is a required property")
-    for f, t in sch["properties"].items():
-        if f not in body:
-            continue
-        v = body[f]
-        nullable = t.endswith("?")
-        t = t.rstrip("?")
-        if v is None:
-            if nullable:
-                continue
-            raise ValidationError(f"None is not of type '{t}' ('{f}')")
-        ok = isinstance(v, _PY_TYPES[t]) and not (t in ("integer", "number") and isinstance(v, bool))
-        if not ok:
-            raise ValidationError(f"{v!r} is not of type '{t}' ('{f}')")
+    try:
+        validate(body, SCHEMAS[schema_name], "body")
+    except SchemaError as e:
+        raise ValidationError(str(e))
     return body
 
 
@@ -142,6 +128,26 @@ def _flask_path(op: Op) -> str:
             conv = "int:" if prm.type == "integer" else ""
             p = p.replace("{" + prm.name + "}", f"<{conv}{prm.name}>")
     return p
+
+
+class ResponseContractError(AssertionError):
+    pass
+
+
+def check_response(op: Op, content, status: int) -> None:
+    """A controller's answer against the document: the status must be one the operation
+    declares and the body must match that status's schema (tests turn this on for every
+    request: ``TH_VALIDATE_RESPONSES``)."""
+    ok, body, errors = RESPONSES[op.handler]
+    if status != ok and status not in errors:
+        raise ResponseContractError(f"{op.method} {op.path}: undeclared status {status}")
+    sch = body if status == ok else SCHEMAS["Message"]
+    if sch is None:
+        return
+    try:
+        validate(json.loads(json.dumps(content, default=str)), sch, f"{op.handler}[{status}]")
+    except SchemaError as e:
+        raise ResponseContractError(str(e))
 
 
 def _make_view(op: Op):
@@ -170,6 +176,8 @@ def _make_view(op: Op):
             content, status = result[0], result[1]
         else:
             content, status = result, 200
+        if current_app.config.get("TH_VALIDATE_RESPONSES"):
+            check_response(op, content, status)
         return Response(json.dumps(content, default=str), status=status, mimetype="application/json")
 
     view.__name__ = f"{op.method.lower()}_{op.handler.replace('.', '_')}"
@@ -218,16 +226,14 @@ def create_app(daemon_obj=None) -> Flask:
 
     @app.route(prefix + "/openapi.json")
     def openapi_json():
-        return jsonify(openapi_document(cfg.api.title, cfg.api.url_prefix, __version__))
+        return jsonify(openapi_document(cfg.api.title, cfg.api.url_prefix, __version__, cfg.api.responses))
 
     @app.route(prefix + "/ui/")
     def api_ui():
-        rows = "".join(f"<tr><td>{o.method}</td><td>{prefix}{o.path}</td><td>{o.auth or 'public'}</td>"
-                       f"<td>{o.handler}</td></tr>" for o in OPERATIONS + EXTRA_OPERATIONS)
-        return (f"<html><head><title>{cfg.api.title}</title></head><body><h1>{cfg.api.title}</h1>"
-                f"<p>OpenAPI document: <a href='{prefix}/openapi.json'>{prefix}/openapi.json</a></p>"
-                f"<table border=1><tr><th>method</th><th>path</th><th>auth</th><th>controller</th></tr>{rows}"
-                f"</table></body></html>")
+        from pathlib import Path
+
+        html = (Path(__file__).with_name("explorer.html")).read_text()
+        return Response(html, mimetype="text/html")
 
     @app.after_request
     def cors(resp):

@@ -50,46 +50,242 @@ def Q(name, t="string", **kw):
     return Param(name, "query", t, **kw)
 
 
-# ---- request body schemas: {field: (type, nullable)} + required
+# ------------------------------------------------------------------------- JSON schemas
+# OpenAPI 3.0 schema objects.  The SAME dicts are rendered into the document and enforced by
+# :func:`validate` (request bodies at runtime; response bodies in tests/test_openapi_contract.py).
+def _t(t: str, **kw) -> dict:
+    return {"type": t, **kw}
+
+
+STR, INT, BOOL, NUM = _t("string"), _t("integer"), _t("boolean"), _t("number")
+DATE_TIME = _t("string", format="date-time", example="2026-01-01T10:00:00.000Z")
+HOUR = _t("string", pattern=r"^([01]?\d|2[0-3]):[0-5]\d$", example="08:30")
+WEEKDAYS = ["Monday", "Tuesday", "Wednesday", "Thursday", "Friday", "Saturday", "Sunday"]
+JOB_STATUSES = ["not_running", "running", "terminated", "unsynchronized", "pending"]
+TASK_STATUSES = ["not_running", "running", "terminated", "unsynchronized"]
+
+
+def nullable(s: dict) -> dict:
+    return {**s, "nullable": True}
+
+
+def ref(name: str) -> dict:
+    return {"$ref": f"#/components/schemas/{name}"}
+
+
+def arr(item: dict, **kw) -> dict:
+    return {"type": "array", "items": item, **kw}
+
+
+def obj(props: dict, required=(), extra: bool = True, **kw) -> dict:
+    d = {"type": "object", "properties": props, **kw}
+    if required:
+        d["required"] = list(required)
+    if not extra:
+        d["additionalProperties"] = False
+    return d
+
+
+def envelope(**fields) -> dict:
+    """``{"msg": ..., <key>: <schema>}`` -- the controllers' usual success body."""
+    return obj({"msg": STR, **fields}, required=["msg", *fields])
+
+
 SCHEMAS: dict[str, dict] = {
-    "UserForm": {"required": ["username", "email", "password"],
-                 "properties": {"username": "string", "email": "string", "password": "string"}},
-    "UserUpdateForm": {"required": ["id"],
-                       "properties": {"id": "integer", "roles": "array", "username": "string", "password": "string",
-                                      "email": "string"}},
-    "UserLoginForm": {"required": ["username", "password"],
-                      "properties": {"username": "string", "password": "string"}},
-    "TaskForm": {"required": ["command", "hostname"],
-                 "properties": {"jobId": "integer", "command": "string", "hostname": "string", "cmdsegments": "object",
-                                "maxRestarts": "integer"}},
-    "TaskUpdateForm": {"required": [], "properties": {"command": "string", "hostname": "string", "cmdsegments": "object",
-                                                    "maxRestarts": "integer"}},
+    # --- request bodies
+    "UserForm": obj({"username": _t("string", minLength=1, maxLength=40, example="foobar"),
+                     "email": _t("string", example="foo@bar.com"),
+                     "password": _t("string", example="difficult_password")},
+                    required=["username", "email", "password"]),
+    "UserUpdateForm": obj({"id": INT, "roles": arr(_t("string", enum=["user", "admin"])),
+                           "username": _t("string", minLength=1, maxLength=40), "password": STR, "email": STR},
+                          required=["id"]),
+    "UserLoginForm": obj({"username": STR, "password": STR}, required=["username", "password"]),
+    "PasswordChangeForm": obj({"oldPassword": STR, "newPassword": STR},  # new: self-service
+                              required=["oldPassword", "newPassword"], extra=False),
+    "CommandSegment": obj({"name": _t("string", minLength=1, maxLength=50), "value": STR}, required=["name"]),
+    "CommandSegments": obj({"envs": arr(ref("CommandSegment")), "params": arr(ref("CommandSegment"))},
+                           extra=False),
+    "TaskForm": obj({"jobId": INT, "command": _t("string", maxLength=400), "hostname": _t("string", maxLength=40),
+                     "cmdsegments": ref("CommandSegments"),
+                     "maxRestarts": _t("integer", minimum=0, maximum=100)},  # new: restart policy
+                    required=["command", "hostname"]),
+    "TaskUpdateForm": obj({"command": _t("string", maxLength=400), "hostname": _t("string", maxLength=40),
+                           "cmdsegments": ref("CommandSegments"),
+                           "maxRestarts": _t("integer", minimum=0, maximum=100)}),
     # new: multi-task launch generator (torchrun / torch TCP ranks / TF2 TF_CONFIG / TF1 ClusterSpec)
-    "TaskGenerateForm": {"required": ["template", "placements"],
-                         "properties": {"template": "string", "command": "string", "module": "string",
-                                        "placements": "array", "masterPort": "integer"}},
-    "JobForm": {"required": ["name", "userId"],
-                "properties": {"name": "string", "description": "string", "userId": "integer", "startAt": "string?",
-                               "stopAt": "string?"}},
-    "JobUpdateForm": {"required": [], "properties": {"name": "string", "description": "string", "startAt": "string?",
-                                                     "stopAt": "string?"}},
-    "GroupForm": {"required": ["name"], "properties": {"name": "string", "isDefault": "boolean"}},
-    "GroupUpdateForm": {"required": [], "properties": {"name": "string", "isDefault": "boolean"}},
-    "RestrictionForm": {"required": ["startsAt", "isGlobal"],
-                        "properties": {"name": "string", "startsAt": "string", "endsAt": "string?", "isGlobal": "boolean"}},
-    "RestrictionUpdateForm": {"required": [], "properties": {"name": "string", "startsAt": "string", "endsAt": "string?",
-                                                             "isGlobal": "boolean"}},
-    "ScheduleForm": {"required": ["scheduleDays", "hourStart", "hourEnd"],
-                     "properties": {"scheduleDays": "array", "hourStart": "string", "hourEnd": "string"}},
-    "ScheduleUpdateForm": {"required": [], "properties": {"scheduleDays": "array", "hourStart": "string",
-                                                          "hourEnd": "string"}},
-    "ReservationForm": {"required": ["title", "description", "resourceId", "userId", "start", "end"],
-                        "properties": {"title": "string", "description": "string", "resourceId": "string",
-                                       "userId": "integer", "start": "string", "end": "string"}},
-    "ReservationUpdateForm": {"required": [], "properties": {"title": "string", "description": "string",
-                                                             "resourceId": "string", "start": "string", "end": "string",
-                                                             "isCancelled": "boolean"}},
+    "TaskGenerateForm": obj({"template": STR, "command": STR, "module": STR,
+                             "masterPort": _t("integer", minimum=1, maximum=65535),
+                             "placements": arr(obj({"hostname": STR, "gpu": _t("integer", minimum=0),
+                                                    "gpus": {"description": "[index, ...] or 'auto:N'"},
+                                                    "gpuCount": _t("integer", minimum=1),
+                                                    "role": _t("string", enum=["chief", "worker", "ps", "evaluator"])},
+                                                   required=["hostname"]), minItems=1)},
+                            required=["template", "placements"]),
+    "JobForm": obj({"name": _t("string", minLength=1, maxLength=40), "description": STR, "userId": INT,
+                    "startAt": nullable(DATE_TIME), "stopAt": nullable(DATE_TIME)}, required=["name", "userId"]),
+    "JobUpdateForm": obj({"name": _t("string", minLength=1, maxLength=40), "description": STR,
+                          "startAt": nullable(DATE_TIME), "stopAt": nullable(DATE_TIME)}),
+    "GroupForm": obj({"name": _t("string", minLength=1, maxLength=40), "isDefault": BOOL}, required=["name"]),
+    "GroupUpdateForm": obj({"name": _t("string", minLength=1, maxLength=40), "isDefault": BOOL}),
+    "RestrictionForm": obj({"name": STR, "startsAt": DATE_TIME, "endsAt": nullable(DATE_TIME), "isGlobal": BOOL},
+                           required=["startsAt", "isGlobal"]),
+    "RestrictionUpdateForm": obj({"name": STR, "startsAt": DATE_TIME, "endsAt": nullable(DATE_TIME),
+                                  "isGlobal": BOOL}),
+    # day names and hours are checked by the controller: an unknown day is a 422 in TensorHive 1.1
+    # (tests/functional/controllers/test_schedule_controller_superuser.py:51-59), not a 400
+    "ScheduleForm": obj({"scheduleDays": arr(_t("string", example="Monday")), "hourStart": _t("string", example="8:00"),
+                         "hourEnd": _t("string", example="16:00")}, required=["scheduleDays", "hourStart", "hourEnd"]),
+    "ScheduleUpdateForm": obj({"scheduleDays": arr(_t("string", example="Monday")),
+                               "hourStart": _t("string", example="8:00"), "hourEnd": _t("string", example="16:00")}),
+    "ReservationForm": obj({"title": _t("string", maxLength=60), "description": _t("string", maxLength=200),
+                            "resourceId": STR, "userId": INT, "start": DATE_TIME, "end": DATE_TIME},
+                           required=["title", "description", "resourceId", "userId", "start", "end"]),
+    "ReservationUpdateForm": obj({"title": _t("string", maxLength=60), "description": _t("string", maxLength=200),
+                                  "resourceId": STR, "start": DATE_TIME, "end": DATE_TIME, "isCancelled": BOOL}),
+    # --- display objects
+    "GroupWithoutUsers": obj({"id": INT, "name": STR, "isDefault": BOOL, "createdAt": DATE_TIME},
+                             required=["name", "isDefault"]),
+    "UserWithoutGroup": obj({"id": INT, "username": STR, "createdAt": DATE_TIME, "roles": arr(STR),
+                             "email": STR}),
+    "UserToDisplay": obj({"id": INT, "username": STR, "createdAt": DATE_TIME, "roles": arr(STR), "email": STR,
+                          "groups": arr(ref("GroupWithoutUsers"))}),
+    "Group": obj({"id": INT, "name": STR, "isDefault": BOOL, "createdAt": DATE_TIME,
+                  "users": arr(ref("UserWithoutGroup"))}, required=["name", "isDefault", "users"]),
+    "Resource": obj({"id": STR, "name": nullable(STR), "hostname": nullable(STR)}),
+    "Schedule": obj({"id": INT, "scheduleDays": arr(_t("string", enum=WEEKDAYS)), "hourStart": HOUR,
+                     "hourEnd": HOUR}, required=["scheduleDays", "hourStart", "hourEnd"]),
+    "Restriction": obj({"id": INT, "name": nullable(STR), "createdAt": DATE_TIME, "startsAt": DATE_TIME,
+                        "endsAt": nullable(DATE_TIME), "isGlobal": BOOL, "schedules": arr(ref("Schedule")),
+                        "groups": arr(ref("GroupWithoutUsers")), "users": arr(ref("UserWithoutGroup")),
+                        "resources": arr(ref("Resource"))},
+                       required=["name", "createdAt", "startsAt", "endsAt", "isGlobal", "schedules"]),
+    "Reservation": obj({"id": INT, "title": STR, "description": STR, "resourceId": STR, "userId": INT,
+                        "userName": nullable(STR), "start": DATE_TIME, "end": DATE_TIME, "createdAt": DATE_TIME,
+                        "isCancelled": BOOL, "gpuUtilAvg": nullable(INT), "memUtilAvg": nullable(INT)},
+                       required=["title", "description", "resourceId", "userId", "userName", "start", "end",
+                                 "isCancelled", "gpuUtilAvg", "memUtilAvg"]),
+    "JobToDisplay": obj({"id": INT, "name": STR, "description": nullable(STR), "userId": INT,
+                         "status": _t("string", enum=JOB_STATUSES), "startAt": nullable(DATE_TIME),
+                         "stopAt": nullable(DATE_TIME), "isQueued": nullable(BOOL),
+                         "tasks": arr(ref("TaskToDisplay"))}),
+    "CommandSegmentToDisplay": obj({"name": STR, "value": nullable(STR), "index": INT}),
+    "TaskToDisplay": obj({"id": INT, "jobId": INT, "hostname": STR, "pid": nullable(INT), "command": STR,
+                          "status": _t("string", enum=TASK_STATUSES),
+                          "cmdsegments": obj({"envs": arr(ref("CommandSegmentToDisplay")),
+                                              "params": arr(ref("CommandSegmentToDisplay"))}),
+                          "fullCommand": STR, "gpuId": nullable(INT), "allocatedGpus": arr(INT),
+                          "maxRestarts": INT, "restarts": INT}),
+    "Metric": obj({"value": nullable(NUM), "unit": nullable(STR)}),
+    "GPUProcess": obj({"pid": INT, "command": nullable(STR), "owner": nullable(STR), "task_id": nullable(STR),
+                       "vram": nullable(NUM)}),
+    "GPU": obj({"name": nullable(STR), "index": nullable(INT), "bdf": nullable(STR), "numa_node": nullable(INT),
+                "metrics": obj({}, additionalProperties=ref("Metric")),
+                "processes": nullable(arr(ref("GPUProcess")))}),
+    "GPUAllData": obj({}, additionalProperties=obj({
+        "GPU": nullable(obj({}, additionalProperties=ref("GPU"))),
+        "CPU": nullable(obj({}, additionalProperties=obj({"name": STR, "index": INT,
+                                                          "metrics": nullable(obj({}, additionalProperties=ref("Metric")))})))}),
+        description="hostname -> {GPU: {uuid: GPU}, CPU: {CPU_<host>: {...}}}"),
+    "GPUInfo": obj({}, additionalProperties=obj({"name": nullable(STR), "index": nullable(INT),
+                                                 "bdf": nullable(STR), "numa_node": nullable(INT)}),
+                   description="uuid -> static GPU facts"),
+    "GPUMetricsInTwoCases": obj({}, additionalProperties=obj({}), description=(
+        "uuid -> {metric: Metric} (all metrics) or uuid -> Metric (metric_type given)")),
+    "CPUMetrics": obj({}, additionalProperties=obj({}), description="CPU_<host> -> {metric: Metric} or Metric"),
+    "GPUProcesses": obj({}, additionalProperties=nullable(arr(ref("GPUProcess"))),
+                        description="uuid -> processes on that GPU"),
+    # --- generic bodies
+    "Message": obj({"msg": STR}, required=["msg"]),
+    "Problem": obj({"detail": STR, "status": INT, "title": STR, "type": STR}, required=["detail", "status"]),
+    "TokenPair": obj({"msg": STR, "access_token": STR, "refresh_token": STR}, required=["access_token"]),
+    # --- new operations
+    "Topology": obj({}, additionalProperties=obj({}), description="hostname -> GPU link/NUMA topology"),
+    "InternalMetrics": obj({}, description="services' loop statistics, request latency p50/p99, snapshot ages"),
+    "Templates": obj({"templates": arr(obj({"name": STR}))}),
+    "TrainingMetrics": obj({"msg": STR, "path": STR, "tokensPerSec": nullable(NUM),
+                            "last": nullable(ref("TrainingPoint")), "series": arr(ref("TrainingPoint"))},
+                           required=["series"]),
+    "TrainingPoint": obj({"step": INT, "loss": NUM, "tokensPerSec": NUM, "world": nullable(INT)}),
 }
+
+
+# ------------------------------------------------------------------------- validation
+class SchemaError(ValueError):
+    pass
+
+
+def _resolve_ref(s: dict) -> dict:
+    while "$ref" in s:
+        s = SCHEMAS[s["$ref"].rsplit("/", 1)[-1]]
+    return s
+
+
+_JSON_TYPES = {"string": (str,), "integer": (int,), "number": (int, float), "boolean": (bool,), "array": (list,),
+               "object": (dict,)}
+
+
+def _check_format(v: str, fmt: str, where: str) -> None:
+    if fmt == "date-time":
+        from ..utils.dates import parse
+
+        try:
+            parse(v)
+        except (ValueError, TypeError):
+            raise SchemaError(f"'{v}' is not a 'date-time' ({where})")
+
+
+def validate(value, schema: dict, where: str = "body") -> None:
+    """Validate ``value`` against an OpenAPI 3.0 schema object (subset: $ref, type, nullable, enum,
+    format date-time, pattern, min/maxLength, minimum/maximum, items/minItems, properties,
+    required, additionalProperties).  Raises :class:`SchemaError` naming the failing location."""
+    import re
+
+    s = _resolve_ref(schema)
+    if value is None:
+        if s.get("nullable"):
+            return
+        raise SchemaError(f"None is not of type '{s.get('type', 'object')}' ({where})")
+    t = s.get("type")
+    if t:
+        ok = isinstance(value, _JSON_TYPES[t]) and not (t in ("integer", "number") and isinstance(value, bool))
+        if not ok:
+            raise SchemaError(f"{value!r} is not of type '{t}' ({where})")
+    if "enum" in s and value not in s["enum"]:
+        raise SchemaError(f"{value!r} is not one of {s['enum']} ({where})")
+    if t == "string":
+        if "minLength" in s and len(value) < s["minLength"]:
+            raise SchemaError(f"{value!r} is too short ({where})")
+        if "maxLength" in s and len(value) > s["maxLength"]:
+            raise SchemaError(f"{value!r} is too long ({where})")
+        if "pattern" in s and not re.search(s["pattern"], value):
+            raise SchemaError(f"{value!r} does not match '{s['pattern']}' ({where})")
+        if "format" in s:
+            _check_format(value, s["format"], where)
+    if t in ("integer", "number"):
+        if "minimum" in s and value < s["minimum"]:
+            raise SchemaError(f"{value!r} is less than the minimum of {s['minimum']} ({where})")
+        if "maximum" in s and value > s["maximum"]:
+            raise SchemaError(f"{value!r} is greater than the maximum of {s['maximum']} ({where})")
+    if t == "array":
+        if "minItems" in s and len(value) < s["minItems"]:
+            raise SchemaError(f"{value!r} has fewer than {s['minItems']} items ({where})")
+        for i, v in enumerate(value):
+            validate(v, s.get("items", {}), f"{where}[{i}]")
+    if t == "object" or "properties" in s:
+        for f in s.get("required", []):
+            if f not in value:
+                raise SchemaError(f"'{f}' is a required property ({where})")
+        props = s.get("properties", {})
+        extra = s.get("additionalProperties", True)
+        for k, v in value.items():
+            if k in props:
+                validate(v, props[k], f"{where}.{k}")
+            elif extra is False:
+                raise SchemaError(f"Additional property '{k}' is not allowed ({where})")
+            elif isinstance(extra, dict):
+                validate(v, extra, f"{where}.{k}")
+
 
 ID = [P("id")]
 
@@ -206,6 +402,8 @@ EXTRA_OPERATIONS: list[Op] = [
        body="TaskGenerateForm", body_name="form", tag="jobs"),
     Op("PUT", "/jobs/{id}/reservation/{reservation_id}", "job.attach_to_reservation", "jwt",      # new
        [P("id"), P("reservation_id"), Q("siblings", "boolean")], tag="jobs"),
+    Op("PUT", "/user/password", "user.change_password", "jwt", body="PasswordChangeForm",         # new
+       body_name="form", tag="users"),
     Op("GET", "/tasks/{id}/training", "task.get_training_metrics", "jwt",                       # new
        ID + [Q("lines", "integer")], tag="tasks"),
 ]
@@ -214,19 +412,130 @@ COMPAT_OPERATION_COUNT = 66
 assert len(OPERATIONS) == COMPAT_OPERATION_COUNT, len(OPERATIONS)
 
 
-def _oa_type(t: str) -> dict:
-    nullable = t.endswith("?")
-    t = t.rstrip("?")
-    d: dict = {"type": t}
-    if t == "array":
-        d["items"] = {"type": "string"}
-    if nullable:
-        d["nullable"] = True
-    return d
+# ------------------------------------------------------------------------- responses
+# handler -> (success status, success body schema, error statuses).  Status sets are a superset
+# of the reference document's (tests/fixtures/reference_openapi_contract.json).
+def _env(key: str, schema_name: str) -> dict:
+    return envelope(**{key: ref(schema_name)})
 
 
-def openapi_document(title: str, prefix: str, version: str) -> dict:
-    """Render the OpenAPI 3.0.3 document for every operation."""
+def _env_list(key: str, schema_name: str) -> dict:
+    return envelope(**{key: arr(ref(schema_name))})
+
+
+_R = ref("Restriction")
+RESPONSES: dict[str, tuple[int, dict | None, tuple[int, ...]]] = {
+    "user.get": (200, arr(ref("UserToDisplay")), (401, 403, 422)),
+    "user.get_by_id": (200, _env("user", "UserToDisplay"), (401, 403, 404, 422, 500)),
+    "user.create": (201, _env("user", "UserToDisplay"), (400, 401, 403, 409, 422, 500)),
+    "user.update": (201, _env("user", "UserToDisplay"), (400, 401, 403, 404, 409, 422, 500)),
+    "user.ssh_signup": (201, _env("user", "UserToDisplay"), (400, 403, 409, 422, 500)),
+    "user.delete": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "user.logout_with_access_token": (200, ref("Message"), (401, 422, 500)),
+    "user.logout_with_refresh_token": (200, ref("Message"), (401, 422, 500)),
+    "user.generate": (200, obj({"access_token": STR}, required=["access_token"]), (401, 422)),
+    "user.login": (200, ref("TokenPair"), (400, 401, 404, 422, 500)),
+    "user.authorized_keys_entry": (200, obj({}), (500,)),
+    "user.change_password": (200, ref("Message"), (400, 401, 403, 422)),
+    "group.get": (200, arr(ref("Group")), (400, 401, 403, 422)),
+    "group.create": (201, _env("group", "Group"), (400, 401, 403, 422, 500)),
+    "group.get_by_id": (200, _env("group", "Group"), (401, 404, 422, 500)),
+    "group.update": (200, _env("group", "Group"), (400, 401, 403, 404, 422, 500)),
+    "group.delete": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "group.add_user": (200, _env("group", "Group"), (401, 403, 404, 409, 422, 500)),
+    "group.remove_user": (200, _env("group", "Group"), (401, 403, 404, 422, 500)),
+    "restriction.get": (200, arr(_R), (400, 401, 403, 422, 500)),
+    "restriction.create": (201, _env("restriction", "Restriction"), (400, 401, 403, 422, 500)),
+    "restriction.update": (200, _env("restriction", "Restriction"), (400, 401, 403, 404, 422, 500)),
+    "restriction.delete": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "schedule.get": (200, arr(ref("Schedule")), (401, 403, 422, 500)),
+    "schedule.create": (201, _env("schedule", "Schedule"), (400, 401, 403, 422, 500)),
+    "schedule.get_by_id": (200, _env("schedule", "Schedule"), (401, 404, 422, 500)),
+    "schedule.update": (200, _env("schedule", "Schedule"), (400, 401, 403, 404, 422, 500)),
+    "schedule.delete": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "job.get_all": (200, _env_list("jobs", "JobToDisplay"), (400, 401, 403, 422, 500)),
+    "job.create": (201, _env("job", "JobToDisplay"), (400, 401, 403, 409, 422, 500)),
+    "job.get_by_id": (200, _env("job", "JobToDisplay"), (401, 403, 404, 422, 500)),
+    "job.update": (200, _env("job", "JobToDisplay"), (400, 401, 403, 404, 422, 500)),
+    "job.delete": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "job.execute": (200, _env("job", "JobToDisplay"), (401, 403, 404, 409, 422, 500)),
+    "job.enqueue": (200, _env("job", "JobToDisplay"), (401, 403, 404, 409, 422, 500)),
+    "job.dequeue": (200, _env("job", "JobToDisplay"), (401, 403, 404, 409, 422, 500)),
+    "job.stop": (200, _env("job", "JobToDisplay"), (401, 403, 404, 409, 422, 500)),
+    "job.add_task": (200, _env("job", "JobToDisplay"), (401, 403, 404, 409, 422, 500)),
+    "job.remove_task": (200, _env("job", "JobToDisplay"), (401, 403, 404, 422, 500)),
+    "task.create": (201, _env("task", "TaskToDisplay"), (400, 401, 403, 404, 409, 422, 500)),
+    "reservation.get": (200, arr(ref("Reservation")), (400, 401, 422, 500)),
+    "reservation.create": (201, _env("reservation", "Reservation"), (400, 401, 403, 422, 500)),
+    "reservation.update": (201, _env("reservation", "Reservation"), (400, 401, 403, 404, 422, 500)),
+    "reservation.delete": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "resource.get": (200, arr(ref("Resource")), (401, 403, 422)),
+    "resource.get_by_id": (200, _env("resource", "Resource"), (401, 404, 422, 500)),
+    "nodes.get_hostnames": (200, arr(STR), (401, 422)),
+    "nodes.get_all_data": (200, ref("GPUAllData"), (401, 422)),
+    "nodes.get_gpu_info": (200, ref("GPUInfo"), (401, 404, 422)),
+    "nodes.get_gpu_metrics": (200, ref("GPUMetricsInTwoCases"), (400, 401, 404, 422)),
+    "nodes.get_cpu_metrics": (200, ref("CPUMetrics"), (400, 401, 404, 422)),
+    "nodes.get_gpu_processes": (200, ref("GPUProcesses"), (401, 404, 422)),
+    "task.get_all": (200, _env_list("tasks", "TaskToDisplay"), (400, 401, 403, 404, 422, 500)),
+    "task.get": (200, _env("task", "TaskToDisplay"), (401, 403, 404, 422, 500)),
+    "task.update": (201, _env("task", "TaskToDisplay"), (400, 401, 403, 404, 422, 500)),
+    "task.destroy": (200, ref("Message"), (401, 403, 404, 422, 500)),
+    "task.get_log": (200, envelope(path=STR, output_lines=arr(STR)), (401, 403, 404, 422, 500)),
+    # new operations
+    "nodes.get_topology": (200, ref("Topology"), (401, 422)),
+    "nodes.get_internal_metrics": (200, ref("InternalMetrics"), (401, 403, 422)),
+    "nodes.get_prometheus": (200, None, ()),
+    "job.get_templates": (200, obj({"msg": STR, "templates": obj({}, additionalProperties=obj({}))}), (401, 422)),
+    "job.generate_tasks": (201, _env_list("tasks", "TaskToDisplay"), (400, 401, 403, 404, 422, 500)),
+    "job.attach_to_reservation": (200, _env("job", "JobToDisplay"), (400, 401, 403, 404, 409, 422, 500)),
+    "task.get_training_metrics": (200, ref("TrainingMetrics"), (401, 403, 404, 422, 500)),
+}
+for _h in ("apply_to_user", "remove_from_user", "apply_to_group", "remove_from_group", "apply_to_resource",
+           "remove_from_resource", "apply_to_resources_by_hostname", "remove_from_resources_by_hostname",
+           "add_schedule", "remove_schedule"):
+    RESPONSES[f"restriction.{_h}"] = (200, _env("restriction", "Restriction"), (400, 401, 403, 404, 409, 422, 500))
+
+_ERROR_TEXT = {400: ("general", "bad_request"), 401: ("general", "unauthorized"), 403: ("general", "unprivileged"),
+               404: None, 409: None, 422: ("general", "auth_error"), 500: ("general", "internal_error")}
+_ERROR_FALLBACK = {404: "Not found", 409: "Conflict with the current state"}
+
+
+def _message(responses: dict | None, keys) -> str | None:
+    cur = responses or {}
+    for k in keys:
+        if not isinstance(cur, dict) or k not in cur:
+            return None
+        cur = cur[k]
+    return cur if isinstance(cur, str) else None
+
+
+def _op_responses(op: Op, messages: dict | None) -> dict:
+    ok, body, errors = RESPONSES[op.handler]
+    entity = op.handler.split(".", 1)[0]
+    out: dict = {}
+    desc = _message(messages, (entity, op.handler.split(".", 1)[1], "success")) or \
+        _message(messages, ("general", "success")) or "OK"
+    out[str(ok)] = {"description": desc}
+    if body is not None:
+        out[str(ok)]["content"] = {"application/json": {"schema": body}}
+    elif op.handler == "nodes.get_prometheus":
+        out[str(ok)]["content"] = {"text/plain": {"schema": STR}}
+    for code in errors:
+        if code == 404:
+            d = _message(messages, (entity, "not_found"))
+        else:
+            keys = _ERROR_TEXT.get(code)
+            d = _message(messages, keys) if keys else None
+        d = d or _ERROR_FALLBACK.get(code, "Error")
+        sch = ref("Problem") if code == 400 else ref("Message")
+        out[str(code)] = {"description": d, "content": {"application/json": {"schema": sch}}}
+    return out
+
+
+def openapi_document(title: str, prefix: str, version: str, messages: dict | None = None) -> dict:
+    """Render the OpenAPI 3.0.3 document for every operation: parameters, request bodies, every
+    response status with its body schema, and the component schemas they reference."""
     paths: dict = {}
     for op in OPERATIONS + EXTRA_OPERATIONS:
         item = paths.setdefault(op.path, {})
@@ -241,25 +550,27 @@ def openapi_document(title: str, prefix: str, version: str) -> dict:
                 sch["items"] = {"type": p.items}
             params.append({"name": p.name, "in": p.where, "required": p.required, "schema": sch})
         entry: dict = {"operationId": f"tensorhive_fixed_amd.controllers.{op.handler}", "tags": [op.tag],
-                       "parameters": params, "responses": {"200": {"description": "OK"}}}
+                       "summary": op.summary or op.handler.replace(".", " ").replace("_", " "),
+                       "parameters": params, "responses": _op_responses(op, messages)}
         if op.auth is None:
             entry["security"] = []
+        else:
+            entry["security"] = [{"Bearer": []}]
+            entry["x-auth"] = op.auth
         if op.body:
             entry["requestBody"] = {"required": True, "x-body-name": op.body_name,
-                                    "content": {"application/json": {"schema": {"$ref": f"#/components/schemas/{op.body}"}}}}
+                                    "content": {"application/json": {"schema": ref(op.body)}}}
         item[op.method.lower()] = entry
-    schemas = {}
-    for name, s in SCHEMAS.items():
-        sch = {"type": "object", "properties": {k: _oa_type(v) for k, v in s["properties"].items()}}
-        if s["required"]:
-            sch["required"] = list(s["required"])
-        schemas[name] = sch
     return {
         "openapi": "3.0.3",
         "info": {"title": title, "version": version},
         "servers": [{"url": f"/{prefix}"}],
         "paths": paths,
-        "components": {"schemas": schemas,
+        "components": {"schemas": SCHEMAS,
+                       "parameters": {
+                           "gpuMetricTypeQuery": {"name": "metric_type", "in": "query", "required": False,
+                                                  "schema": {"type": "string", "enum": GPU_METRICS}},
+                           "cpuMetricTypeQuery": {"name": "metric_type", "in": "query", "required": False,
+                                                  "schema": {"type": "string", "enum": CPU_METRICS}}},
                        "securitySchemes": {"Bearer": {"type": "http", "scheme": "bearer", "bearerFormat": "JWT"}}},
-        "security": [{"Bearer": []}],
     }

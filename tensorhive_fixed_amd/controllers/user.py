@@ -97,6 +97,18 @@ def update(newValues: dict):
     return {"msg": M("user.update.success"), "reservation": d, "user": d}, 201
 
 
+@guarded(not_found="user.not_found", assertion="user.update.failure.invalid")
+def change_password(form: dict):
+    """Self-service password change (new; ``PUT /user`` is admin-only in TensorHive 1.1, which left
+    non-admin users without a way to change their own password).  The old password must match."""
+    user = User.get(me())
+    if not User.verify_hash(form["oldPassword"], user.password):
+        return {"msg": M("user.login.failure.credentials")}, 403
+    user.password = form["newPassword"]
+    user.save()
+    return {"msg": M("user.update.success")}, 200
+
+
 @guarded(not_found="user.not_found")
 def delete(id: int):
     if id == me():

@@ -60,7 +60,11 @@ def configure(uri: str | None = None):
         else:
             if uri.startswith("sqlite:///"):
                 Path(uri[len("sqlite:///"):]).expanduser().parent.mkdir(parents=True, exist_ok=True)
-            eng = create_engine(uri, connect_args={"check_same_thread": False, "timeout": 30})
+            # one scoped session (= one pooled connection) per thread: API request threads, the
+            # services and launch fan-outs run at once, so the pool is sized well above
+            # SQLAlchemy's 5+10 default (SQLite connections are cheap file handles)
+            eng = create_engine(uri, connect_args={"check_same_thread": False, "timeout": 30},
+                                pool_size=32, max_overflow=64, pool_timeout=60)
             event.listen(eng, "connect", _wal_pragma)
         event.listen(eng, "connect", _fk_pragma)
         db_session.configure(bind=eng)

@@ -105,6 +105,7 @@ def app(daemon):
 
     a = create_app(daemon)
     a.config["TH_REMOVE_SESSION"] = False
+    a.config["TH_VALIDATE_RESPONSES"] = True  # every answer is checked against the OpenAPI document
     return a
 
 
