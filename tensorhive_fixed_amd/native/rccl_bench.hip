@@ -2,7 +2,7 @@
 //
 // One process drives every visible GPU (ncclCommInitAll) so it runs without a launcher:
 //   rccl-bench [--gpus N] [--min BYTES] [--max BYTES] [--iters K] [--op allreduce|reducescatter|allgather|all]
-//              [--direct]
+//              [--direct] | --check-virtual-peers P [--min BYTES]
 // For each bf16 message size it reports algorithm bandwidth (bytes/time) and bus bandwidth
 // (allreduce: 2(n-1)/n x algbw; reduce-scatter / all-gather: (n-1)/n x algbw) as JSON lines.
 // `--direct` adds a one-shot peer-to-peer all-reduce HIP kernel for comparison: every GPU reads
@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 
 #include <chrono>
@@ -54,8 +55,71 @@ __global__ void direct_allreduce(u16** bufs, int npeers, long lo, long hi) {
   }
 }
 
+// Correctness check of direct_allreduce without N GPUs: `vpeers` buffers on ONE device stand in
+// for the peers (the kernel only sees an array of peer pointers, so the indexing, slicing and
+// f32 accumulation are exactly what runs across xGMI).  Every slice is reduced by its own launch,
+// as each GPU would; the result must equal the host's f32 sum rounded to bf16, bit for bit, in
+// every peer buffer.  Prints one JSON line; exit code 0 iff it matches.
+static u16 h_f2b(float f) {  // round-to-nearest-even, as (__bf16)f
+  unsigned u;
+  memcpy(&u, &f, 4);
+  u += 0x7fff + ((u >> 16) & 1);
+  return (u16)(u >> 16);
+}
+static float h_b2f(u16 b) {
+  unsigned u = (unsigned)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static int check_direct(int vpeers, long count) {
+  CK(hipSetDevice(0));
+  std::vector<u16*> bufs(vpeers);
+  std::vector<std::vector<u16>> host(vpeers, std::vector<u16>(count));
+  for (int p = 0; p < vpeers; ++p) {
+    for (long i = 0; i < count; ++i)  // distinct, exactly representable-ish values per peer and index
+      host[p][i] = h_f2b(0.001f * (float)((i * 7 + p * 13) % 1024) - 0.37f * (float)(p + 1));
+    CK(hipMalloc((void**)&bufs[p], count * sizeof(u16)));
+    CK(hipMemcpy(bufs[p], host[p].data(), count * sizeof(u16), hipMemcpyHostToDevice));
+  }
+  u16** dptrs = nullptr;
+  CK(hipMalloc((void**)&dptrs, sizeof(u16*) * vpeers));
+  CK(hipMemcpy(dptrs, bufs.data(), sizeof(u16*) * vpeers, hipMemcpyHostToDevice));
+  const long slice = (count + vpeers - 1) / vpeers;
+  for (int r = 0; r < vpeers; ++r) {
+    const long lo = r * slice, hi = lo + slice < count ? lo + slice : count;
+    if (lo < hi) direct_allreduce<<<256, 256>>>(dptrs, vpeers, lo, hi);
+  }
+  CK(hipGetLastError());
+  CK(hipDeviceSynchronize());
+  long bad = 0;
+  double max_err = 0.0;
+  std::vector<u16> got(count);
+  for (int p = 0; p < vpeers; ++p) {
+    CK(hipMemcpy(got.data(), bufs[p], count * sizeof(u16), hipMemcpyDeviceToHost));
+    for (long i = 0; i < count; ++i) {
+      float s = 0.f;
+      for (int q = 0; q < vpeers; ++q) s += h_b2f(host[q][i]);
+      const u16 want = h_f2b(s);
+      if (got[i] != want) {
+        ++bad;
+        const double e = fabs((double)h_b2f(got[i]) - (double)h_b2f(want));
+        max_err = e > max_err ? e : max_err;
+      }
+    }
+  }
+  printf("{\"check\":\"direct_allreduce\",\"virtual_peers\":%d,\"elements\":%ld,\"mismatches\":%ld,"
+         "\"max_abs_err\":%g,\"ok\":%s}\n", vpeers, count, bad, max_err, bad == 0 ? "true" : "false");
+  fflush(stdout);
+  for (int p = 0; p < vpeers; ++p) CK(hipFree(bufs[p]));
+  CK(hipFree(dptrs));
+  return bad == 0 ? 0 : 3;
+}
+
 int main(int argc, char** argv) {
   int ngpu = 0, iters = 20;
+  int vpeers = 0;
   long mn = 8l << 20, mx = 1l << 30;
   std::string op = "all";
   bool direct = false;
@@ -66,7 +130,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--iters") && i + 1 < argc) iters = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--op") && i + 1 < argc) op = argv[++i];
     else if (!strcmp(argv[i], "--direct")) direct = true;
+    else if (!strcmp(argv[i], "--check-virtual-peers") && i + 1 < argc) vpeers = atoi(argv[++i]);
   }
+  if (vpeers > 0) return check_direct(vpeers, (mn / 2) + 37);  // odd length: ragged last slice
   int avail = 0;
   CK(hipGetDeviceCount(&avail));
   if (ngpu <= 0 || ngpu > avail) ngpu = avail;

@@ -51,13 +51,16 @@ struct Gpu {
   double hbm_gbps = -1;
 };
 
-// GB/s per unit/s of mem_activity_acc on MI355X, fitted against timed device streams (add 5.78 TB/s,
-// copy 5.01 TB/s, half-duty add 2.89 TB/s: 0.0938 / 0.0973 / 0.0945; profiles/r02_telemetry/
-// hbm_calibration.jsonl).  Override with TENSORHIVE_HBM_GBPS_PER_ACC.
+// GB/s per unit/s of mem_activity_acc on MI355X, fitted against timed device streams on two boxes:
+// add 5.78 TB/s, copy 5.01 TB/s, half-duty add 2.89 TB/s -> 0.0938 / 0.0973 / 0.0945
+// (profiles/r02_telemetry/hbm_calibration.jsonl); copy 4.80 TB/s on a second box -> 0.0820
+// (gpu_tests_fullwidth_hbm_probe.log).  The accumulator counts UMC activity, not bytes, so the
+// factor moves with the box and the access mix; 0.0897 is the minimax fit (max error 8.5 % over
+// these four).  Override with TENSORHIVE_HBM_GBPS_PER_ACC.
 double hbm_gbps_per_acc() {
   static double k = [] {
     const char* e = getenv("TENSORHIVE_HBM_GBPS_PER_ACC");
-    return (e && *e) ? atof(e) : 0.0952;
+    return (e && *e) ? atof(e) : 0.0897;
   }();
   return k;
 }

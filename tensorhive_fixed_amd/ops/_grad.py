@@ -9,7 +9,8 @@ communication bucket: the bucket IS the gradient.  After writing, the store is t
 parameter is ready so it can launch that bucket's collective while backward continues.
 
 Parameters that are not owned by a store (unit tests, plain use) get an ordinary returned
-gradient instead.
+gradient instead.  With an f32 gradient buffer (``TH_GRAD_FP32=1``) the gradient is produced in
+the compute dtype and added into the f32 ``main_grad`` (accumulation and reduction in f32).
 """
 from __future__ import annotations
 
@@ -30,7 +31,17 @@ def deliver(weight: torch.Tensor, write: Callable[[torch.Tensor, bool], None],
     if mg is None:
         return make()
     store = weight.th_store
-    write(mg, store.accumulating)
+    if mg.dtype != weight.dtype:
+        # f32 main gradients (TH_GRAD_FP32): the GEMM writes this micro-batch's gradient in the
+        # compute dtype, the accumulation across micro-batches and the reduction run in f32
+        g = make()
+        if store.accumulating:
+            mg.add_(g.view_as(mg))
+        else:
+            mg.copy_(g.view_as(mg))
+        del g
+    else:
+        write(mg, store.accumulating)
     store.mark_ready(weight)
     return None
 

@@ -39,6 +39,8 @@ _SIGS: dict[str, list] = {
     "th_rope_inplace": [P, P, P, L, I, I, I, I, F, P],
     "th_sumsq_bf16": [P, L, P, P, I, P],
     "th_adamw_step": [P, P, P, P, P, L, F, F, F, F, F, I, F, P, F, P],
+    "th_adamw_step_f32g": [P, P, P, P, P, L, F, F, F, F, F, I, F, P, F, P],
+    "th_sumsq_f32": [P, L, P, P, I, P],
     "th_ce_fwd_bwd": [P, L, P, P, P, L, I, F, I, P],
     "th_flash_attn_fwd": [P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, I, P],
     "th_flash_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, I, P],

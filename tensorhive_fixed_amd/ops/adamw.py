@@ -16,7 +16,8 @@ def grad_sumsq_(grad: torch.Tensor, out: torch.Tensor, accumulate: bool = False)
     n = grad.numel()
     if grad.is_cuda:
         ws = torch.empty(2048, device=grad.device, dtype=torch.float32)
-        _lib.call("th_sumsq_bf16", grad.data_ptr(), n, ws.data_ptr(), out.data_ptr(), int(accumulate),
+        fn = "th_sumsq_f32" if grad.dtype == torch.float32 else "th_sumsq_bf16"
+        _lib.call(fn, grad.data_ptr(), n, ws.data_ptr(), out.data_ptr(), int(accumulate),
                   _lib.stream_ptr(grad.device))
     else:
         s = grad.float().pow(2).sum()
@@ -33,9 +34,11 @@ def adamw_flat_(param: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor
         if t.numel() != n:
             raise ValueError("adamw_flat_: all flat ranges must have the same length")
     if param.is_cuda:
-        if n % 8 or param.dtype != torch.bfloat16 or grad.dtype != torch.bfloat16 or master.dtype != torch.float32:
-            raise ValueError("adamw kernel needs bf16 param/grad, f32 state and n % 8 == 0")
-        _lib.call("th_adamw_step", param.data_ptr(), master.data_ptr(), exp_avg.data_ptr(),
+        if n % 8 or param.dtype != torch.bfloat16 or grad.dtype not in (torch.bfloat16, torch.float32) \
+                or master.dtype != torch.float32:
+            raise ValueError("adamw kernel needs bf16 param, bf16/f32 grad, f32 state and n % 8 == 0")
+        fn = "th_adamw_step_f32g" if grad.dtype == torch.float32 else "th_adamw_step"
+        _lib.call(fn, param.data_ptr(), master.data_ptr(), exp_avg.data_ptr(),
                   exp_avg_sq.data_ptr(), grad.data_ptr(), n, float(lr), float(beta1), float(beta2),
                   float(eps), float(weight_decay), int(step), float(grad_scale),
                   None if norm_sq is None else norm_sq.data_ptr(), float(clip),

@@ -62,8 +62,12 @@ class _LinearCE(torch.autograd.Function):
         dh = torch.empty_like(h2)
         loss_sum = torch.zeros((), device=h2.device, dtype=torch.float32)
         mg = getattr(w, "main_grad", None)
-        acc = mg.view_as(w) if mg is not None else torch.zeros(w.shape, device=w.device, dtype=torch.float32)
-        first_acc = mg is not None and not w.th_store.accumulating
+        f32_main = mg is not None and mg.dtype != w.dtype  # TH_GRAD_FP32: GEMMs write bf16, added in f32
+        if f32_main:
+            acc = torch.empty(w.shape, device=w.device, dtype=w.dtype)
+        else:
+            acc = mg.view_as(w) if mg is not None else torch.zeros(w.shape, device=w.device, dtype=torch.float32)
+        first_acc = mg is not None and (f32_main or not w.th_store.accumulating)
         # dh = dlogits @ W in the K-contiguous form (see ops/linear.py): one transpose of W per call
         w_kn = transpose(w).t() if (h2.is_cuda and _DGRAD_NT) else w
         for i, s0 in enumerate(range(0, T, chunk)):
@@ -88,6 +92,9 @@ class _LinearCE(torch.autograd.Function):
                 acc.addmm_(logits.t().float(), hc.float())
             del logits
         del w_kn
+        if f32_main:
+            (mg.add_ if w.th_store.accumulating else mg.copy_)(acc.view_as(mg))
+            del acc
         if mg is not None:
             w.th_store.mark_ready(w)
             ctx.gw = None

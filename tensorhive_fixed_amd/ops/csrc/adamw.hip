@@ -9,18 +9,31 @@
 // there is no host synchronisation anywhere in the step (graph-capturable).
 #include "th_common.h"
 
-__global__ __launch_bounds__(256) void sumsq_bf16_kernel(const ushort* __restrict__ g, long n8,
-                                                         float* __restrict__ partial) {
+// 8 consecutive gradient values as f32, from the bf16 (default) or the f32 (TH_GRAD_FP32) buffer
+__device__ __forceinline__ void load_grad8(const ushort* __restrict__ g, long i, float out[8]) {
+  const ushort8 v = reinterpret_cast<const ushort8*>(g)[i];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = bf2f(v[j]);
+}
+__device__ __forceinline__ void load_grad8(const float* __restrict__ g, long i, float out[8]) {
+  const float4v a = reinterpret_cast<const float4v*>(g)[2 * i], b = reinterpret_cast<const float4v*>(g)[2 * i + 1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[j] = a[j];
+    out[4 + j] = b[j];
+  }
+}
+
+template <typename G>
+__global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ g, long n8, float* __restrict__ partial) {
   __shared__ float red[16];
   float acc = 0.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
-    const ushort8 v = reinterpret_cast<const ushort8*>(g)[i];
+    float v[8];
+    load_grad8(g, i, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = bf2f(v[j]);
-      acc += f * f;
-    }
+    for (int j = 0; j < 8; ++j) acc += v[j] * v[j];
   }
   acc = block_sum(acc, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = acc;
@@ -35,9 +48,10 @@ __global__ void final_sum_kernel(const float* __restrict__ partial, int np, floa
   if (threadIdx.x == 0) out[0] = accumulate ? out[0] + acc : acc;
 }
 
+template <typename G>
 __global__ __launch_bounds__(256) void adamw_kernel(
     ushort* __restrict__ p, float* __restrict__ master, float* __restrict__ m,
-    float* __restrict__ v, const ushort* __restrict__ g, long n8, float lr, float b1, float b2,
+    float* __restrict__ v, const G* __restrict__ g, long n8, float lr, float b1, float b2,
     float eps, float wd, float bc1, float bc2, float grad_scale, const float* __restrict__ norm_sq,
     float clip) {
   float scale = grad_scale;
@@ -49,7 +63,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(
   const float inv_sqrt_bc2 = rsqrtf(bc2);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
-    const ushort8 gv = reinterpret_cast<const ushort8*>(g)[i];
+    float gv[8];
+    load_grad8(g, i, gv);
     float4v* mp = reinterpret_cast<float4v*>(master) + 2 * i;
     float4v* m1 = reinterpret_cast<float4v*>(m) + 2 * i;
     float4v* v1 = reinterpret_cast<float4v*>(v) + 2 * i;
@@ -58,7 +73,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int h = j >> 2, k = j & 3;
-      const float gr = bf2f(gv[j]) * scale;
+      const float gr = gv[j] * scale;
       float mm = b1 * mw[h][k] + (1.f - b1) * gr;
       float vv = b2 * vw[h][k] + (1.f - b2) * gr * gr;
       float pp = pw[h][k] * (1.f - lr * wd);
@@ -87,7 +102,15 @@ extern "C" int th_sumsq_bf16(const void* g, long n, float* ws, float* out, int a
                              hipStream_t s) {
   if (n % 8 != 0 || n <= 0) return -1;
   const unsigned gs = grid_cap(n / 8);
-  sumsq_bf16_kernel<<<gs, 256, 0, s>>>((const ushort*)g, n / 8, ws);
+  sumsq_kernel<ushort><<<gs, 256, 0, s>>>((const ushort*)g, n / 8, ws);
+  final_sum_kernel<<<1, 1024, 0, s>>>(ws, (int)gs, out, accumulate);
+  TH_CHECK_LAUNCH();
+}
+
+extern "C" int th_sumsq_f32(const float* g, long n, float* ws, float* out, int accumulate, hipStream_t s) {
+  if (n % 8 != 0 || n <= 0) return -1;
+  const unsigned gs = grid_cap(n / 8);
+  sumsq_kernel<float><<<gs, 256, 0, s>>>(g, n / 8, ws);
   final_sum_kernel<<<1, 1024, 0, s>>>(ws, (int)gs, out, accumulate);
   TH_CHECK_LAUNCH();
 }
@@ -98,7 +121,19 @@ extern "C" int th_adamw_step(void* p, float* master, float* m, float* v, const v
   if (n % 8 != 0 || n <= 0 || step < 1) return -1;
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2 = 1.f - powf(b2, (float)step);
-  adamw_kernel<<<grid_cap(n / 8), 256, 0, s>>>((ushort*)p, master, m, v, (const ushort*)g, n / 8, lr,
-                                               b1, b2, eps, wd, bc1, bc2, grad_scale, norm_sq, clip);
+  adamw_kernel<ushort><<<grid_cap(n / 8), 256, 0, s>>>((ushort*)p, master, m, v, (const ushort*)g, n / 8, lr,
+                                                       b1, b2, eps, wd, bc1, bc2, grad_scale, norm_sq, clip);
+  TH_CHECK_LAUNCH();
+}
+
+// Same step reading an f32 gradient buffer (TH_GRAD_FP32): 34 B/param instead of 28.
+extern "C" int th_adamw_step_f32g(void* p, float* master, float* m, float* v, const float* g, long n,
+                                  float lr, float b1, float b2, float eps, float wd, int step,
+                                  float grad_scale, const float* norm_sq, float clip, hipStream_t s) {
+  if (n % 8 != 0 || n <= 0 || step < 1) return -1;
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  adamw_kernel<float><<<grid_cap(n / 8), 256, 0, s>>>((ushort*)p, master, m, v, g, n / 8, lr, b1, b2, eps, wd,
+                                                      bc1, bc2, grad_scale, norm_sq, clip);
   TH_CHECK_LAUNCH();
 }

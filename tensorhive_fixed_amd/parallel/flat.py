@@ -15,6 +15,10 @@ MI355X-first data-parallel design (no torch DDP wrapper, no per-tensor grads):
   larger collectives keep RCCL's channels busy.
 * Averaging is folded into the optimizer (``grad_scale = 1/world``); the fused flat AdamW then
   updates the whole model with one kernel per parameter group.
+* ``grad_dtype=float32`` (``TH_GRAD_FP32=1``): the gradient buffer, the micro-batch accumulation
+  and the RCCL reduction are f32 (twice the gradient bytes on the wire; +16 GB for 8B params);
+  the default keeps them bf16.  tests/test_flat_ddp.py bounds the bf16 path's error against the
+  f32 path at world 8 with 4 accumulated micro-batches.
 
 ``shard=True`` (ZeRO-1, the default of the training payload when world > 1) keeps the same flat
 buffers and buckets but distributes the optimizer:
@@ -73,9 +77,13 @@ class FlatParamStore:
 
     def __init__(self, params_in_backward_order: list[tuple[str, torch.nn.Parameter, bool]],
                  device: torch.device, dtype: torch.dtype = torch.bfloat16,
-                 process_group=None, bucket_mb: float = 256.0, shard: bool = False):
+                 process_group=None, bucket_mb: float = 256.0, shard: bool = False,
+                 grad_dtype: torch.dtype | None = None):
         self.device = torch.device(device)
         self.dtype = dtype
+        if grad_dtype is None:
+            grad_dtype = torch.float32 if os.environ.get("TH_GRAD_FP32", "0") == "1" else dtype
+        self.grad_dtype = grad_dtype
         self.pg = process_group
         initialized = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(process_group) if initialized else 1
@@ -88,7 +96,7 @@ class FlatParamStore:
         self.decay_numel = max([o + p.numel() for (_, p, d), o in zip(ordered, offs) if d], default=0)
         self.decay_numel = _round_up(self.decay_numel, _ALIGN)
         self.param_buf = torch.zeros(self.numel, device=self.device, dtype=dtype)
-        self.grad_buf = torch.zeros(self.numel, device=self.device, dtype=dtype)
+        self.grad_buf = torch.zeros(self.numel, device=self.device, dtype=grad_dtype)
         self.names: list[str] = []
         self.params: list[torch.nn.Parameter] = []
         self.offsets: dict[int, int] = {}
