@@ -84,3 +84,58 @@ export function validReservationRange(start, end) {
   if (m > MAX_RESERVATION_MIN) return "a reservation lasts at most 8 days";
   return null;
 }
+
+// ---------------------------------------------------------------- calendar selection
+// The calendar is a grid of columns (day d, GPU g) x rows (slot s of `slotMin` minutes).  A drag
+// from cell a to cell b selects the GPUs between the two columns' GPUs (in display order) and the
+// time between the earlier cell's start and the later cell's end, even across days
+// (reference FullCalendar.vue:151 `select` callback + FullCalendarReserve.vue).
+export function dragSelection(a, b, dayStarts, gpuIds, slotMin) {
+  const t = c => new Date(dayStarts[c.day]).getTime() + c.slot * slotMin * 60000;
+  const ta = t(a), tb = t(b);
+  const lo = Math.min(ta, tb), hi = Math.max(ta, tb) + slotMin * 60000;
+  const g0 = Math.min(a.gpu, b.gpu), g1 = Math.max(a.gpu, b.gpu);
+  return { start: new Date(lo), end: new Date(hi), gpus: gpuIds.slice(g0, g1 + 1) };
+}
+
+// Lay reservations of one column (one GPU, one day) out as [top, height] fractions of the day;
+// overlapping cancelled entries keep their slot (they are drawn struck out).
+export function layoutDay(reservations, dayStart) {
+  const d0 = new Date(dayStart).getTime(), d1 = d0 + 864e5;
+  return reservations
+    .map(r => ({ r, s: Math.max(d0, new Date(r.start).getTime()), e: Math.min(d1, new Date(r.end).getTime()) }))
+    .filter(x => x.e > x.s)
+    .map(x => ({ r: x.r, top: (x.s - d0) / 864e5, height: (x.e - x.s) / 864e5 }));
+}
+
+// Does the set of restrictions of a user (GET /restrictions?user_id=..&include_user_groups=true)
+// allow GPU `uuid` over the whole window [start, end)?  Mirrors core/verifier.py: a restriction
+// covers the GPU if it is global or lists it; the window must be inside the union of the covering
+// restrictions' [startsAt, endsAt) x schedule windows.  Checked per `stepMin` minutes.
+export function restrictionCovers(r, uuid) {
+  return r.isGlobal || (r.resources || []).some(x => x.id === uuid);
+}
+
+export function restrictionAllowsAt(r, t) {
+  const x = new Date(t).getTime();
+  if (x < new Date(r.startsAt).getTime()) return false;
+  if (r.endsAt && x >= new Date(r.endsAt).getTime()) return false;
+  const sch = r.schedules || [];
+  return !sch.length || sch.some(s => inSchedule(s, t));
+}
+
+export function allowedWindow(restrictions, uuid, start, end, stepMin = 15) {
+  const cover = restrictions.filter(r => restrictionCovers(r, uuid));
+  if (!cover.length) return false;
+  for (let t = new Date(start).getTime(); t < new Date(end).getTime(); t += stepMin * 60000)
+    if (!cover.some(r => restrictionAllowsAt(r, t))) return false;
+  return true;
+}
+
+// Mean of the reservation usage averages that are known (gpuUtilAvg / memUtilAvg, C67).
+export function usageSummary(reservations) {
+  const g = reservations.map(r => r.gpuUtilAvg).filter(v => v !== null && v !== undefined);
+  const m = reservations.map(r => r.memUtilAvg).filter(v => v !== null && v !== undefined);
+  const avg = a => a.length ? Math.round(a.reduce((x, y) => x + y, 0) / a.length) : null;
+  return { gpuUtilAvg: avg(g), memUtilAvg: avg(m), samples: g.length };
+}

@@ -4,6 +4,7 @@ import json
 import re
 import shutil
 import subprocess
+from pathlib import Path
 
 import pytest
 from click.testing import CliRunner
@@ -20,33 +21,160 @@ def test_web_app_serves_spa_and_config(cfg):
     r = c.get("/")
     assert r.status_code == 200 and b"TensorHive" in r.data
     r = c.get("/reservations/deep/link")  # SPA fallback
-    assert r.status_code == 200 and b"<script>" in r.data
+    assert r.status_code == 200 and b'<script type="module" src="/js/main.js">' in r.data
+    r = c.get("/js/main.js")
+    assert r.status_code == 200 and "javascript" in r.mimetype and b"route()" in r.data
     assert (STATIC / "index.html").exists()
 
 
-@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
-def test_spa_script_parses(tmp_path):
-    from tensorhive_fixed_amd.app.server import STATIC
+SPA_JS = sorted((Path(__file__).resolve().parents[1] / "tensorhive_fixed_amd" / "app" / "static" / "js").glob("*.js"))
+_CALL = re.compile(r'(?:call|raw)\(\s*"(GET|POST|PUT|DELETE)",\s*(["`])(/[^"`]*)\2')
 
-    js = re.search(r"<script>(.*)</script>", (STATIC / "index.html").read_text(), re.S).group(1)
-    (tmp_path / "spa.js").write_text(js)
-    r = subprocess.run(["node", "--check", str(tmp_path / "spa.js")], capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr
+
+def _spa_calls() -> set[tuple[str, str]]:
+    """(method, path regex) of every API request in the dashboard modules; `${...}` is one segment."""
+    out = set()
+    for f in SPA_JS:
+        for m in _CALL.finditer(f.read_text()):
+            path = re.sub(r"\$\{[^}]*\}", "\x00", m.group(3))
+            out.add((m.group(1), "^" + re.escape(path).replace("\x00", "[^/?]+") + "$"))
+    return out
+
+
+def _instance(path: str) -> str:
+    return re.sub(r"\{[^}]+\}", "1", path)
+
+
+def test_spa_modules_parse():
+    assert {f.name for f in SPA_JS} >= {"main.js", "api.js", "ui.js", "nodes.js", "reservations.js", "jobs.js",
+                                        "admin.js", "time.js", "launch.js", "chart.js"}
+    if shutil.which("node") is None:
+        pytest.skip("node not installed")
+    for f in SPA_JS:
+        r = subprocess.run(["node", "--check", str(f)], capture_output=True, text=True)
+        assert r.returncode == 0, (f.name, r.stderr)
 
 
 def test_spa_uses_only_known_endpoints():
-    """Every API path the dashboard calls exists in the spec (catches drift between the two)."""
+    """Every API request the dashboard makes is an operation of the spec (catches drift)."""
     from tensorhive_fixed_amd.api.spec import EXTRA_OPERATIONS, OPERATIONS
-    from tensorhive_fixed_amd.app.server import STATIC
 
-    src = (STATIC / "index.html").read_text()
-    pats = [re.compile("^" + re.sub(r"\{[^}]+\}", "[^/?]+", op.path) + "$") for op in list(OPERATIONS) + list(EXTRA_OPERATIONS)]
-    used = set(re.findall(r'call\("(?:GET|POST|PUT|DELETE)", [`"](/[^`"?]*)', src))
-    used |= set(re.findall(r'"(/(?:users|groups|restrictions|schedules|resources))"', src))
-    assert used
-    for u in used:
-        u = re.sub(r"\$\{[^}]+\}", "X", u.replace("${pick.value}", "users/X"))
-        assert any(p.match(u) for p in pats), u
+    ops = [(op.method, _instance(op.path)) for op in list(OPERATIONS) + list(EXTRA_OPERATIONS)]
+    calls = _spa_calls()
+    assert len(calls) > 40
+    for method, rx in calls:
+        assert any(m == method and re.match(rx, p) for m, p in ops), (method, rx)
+
+
+# (method, operation) pairs the reference Vue SPA issues (tensorhive/app/web/dev/src: api/*.js,
+# components/**/*.vue, main.js); extracted once from its api.request(...) calls.  The dead
+# /tasks/{id}/spawn|terminate calls of TasksOverview.vue (no such operations in its spec) are left out.
+REFERENCE_SPA_OPERATIONS = [
+    ("DELETE", "/groups/{id}"), ("DELETE", "/reservations/{id}"), ("DELETE", "/restrictions/{id}"),
+    ("DELETE", "/tasks/{id}"), ("DELETE", "/user/delete/{id}"), ("DELETE", "/user/logout"),
+    ("DELETE", "/user/logout/refresh_token"), ("DELETE", "/jobs/{job_id}/tasks/{task_id}"), ("DELETE", "/jobs/{id}"),
+    ("GET", "/groups"), ("GET", "/jobs"), ("GET", "/jobs/{id}"), ("GET", "/jobs/{id}/execute"), ("GET", "/jobs/{id}/stop"),
+    ("GET", "/nodes/{hostname}/gpu/metrics"), ("GET", "/nodes/{hostname}/cpu/metrics"), ("GET", "/nodes/hostnames"),
+    ("GET", "/nodes/metrics"), ("GET", "/reservations"), ("GET", "/resources"), ("GET", "/restrictions"),
+    ("GET", "/tasks"), ("GET", "/tasks/{id}"), ("GET", "/tasks/{id}/log"), ("GET", "/user/authorized_keys_entry"),
+    ("GET", "/users"), ("GET", "/users/{id}"), ("GET", "/user/refresh"),
+    ("POST", "/groups"), ("POST", "/reservations"), ("POST", "/restrictions"), ("POST", "/schedules"),
+    ("POST", "/user/create"), ("POST", "/user/login"), ("POST", "/user/ssh_signup"), ("POST", "/jobs/{job_id}/tasks"),
+    ("POST", "/jobs"),
+    ("PUT", "/groups/{id}"), ("PUT", "/groups/{group_id}/users/{user_id}"), ("DELETE", "/groups/{group_id}/users/{user_id}"),
+    ("PUT", "/reservations/{id}"), ("PUT", "/restrictions/{id}"), ("PUT", "/restrictions/{restriction_id}/users/{user_id}"),
+    ("PUT", "/restrictions/{restriction_id}/groups/{group_id}"),
+    ("PUT", "/restrictions/{restriction_id}/resources/{resource_uuid}"),
+    ("PUT", "/restrictions/{restriction_id}/schedules/{schedule_id}"), ("PUT", "/tasks/{id}"), ("PUT", "/user"),
+    ("PUT", "/jobs/{id}/dequeue"), ("PUT", "/jobs/{id}/enqueue"), ("PUT", "/jobs/{job_id}/tasks/{task_id}"),
+    ("PUT", "/jobs/{id}"),
+]
+
+
+def test_spa_covers_every_reference_spa_operation():
+    """The dashboard reaches every operation the reference SPA used, plus the new ones."""
+    calls = _spa_calls()
+    extra = [("PUT", "/user/password"), ("PUT", "/schedules/{id}"), ("DELETE", "/schedules/{id}"),
+             ("POST", "/jobs/{id}/tasks/generate"), ("PUT", "/jobs/{id}/reservation/{reservation_id}"),
+             ("GET", "/tasks/{id}/training"), ("GET", "/jobs/templates"), ("GET", "/nodes/topology"),
+             ("GET", "/nodes/{hostname}/gpu/processes"), ("PUT", "/restrictions/{restriction_id}/hosts/{hostname}"),
+             ("DELETE", "/restrictions/{restriction_id}/users/{user_id}"), ("GET", "/schedules")]
+    missing = [(m, p) for m, p in REFERENCE_SPA_OPERATIONS + extra
+               if not any(cm == m and re.match(rx, _instance(p)) for cm, rx in calls)]
+    assert not missing, missing
+
+
+def _node_eval(tmp_path, script: str):
+    if shutil.which("node") is None:
+        pytest.skip("node not installed")
+    js = SPA_JS[0].parent
+    f = tmp_path / "t.mjs"
+    f.write_text(script.replace("@JS@", js.as_uri()))
+    r = subprocess.run(["node", str(f)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_spa_launch_previews_match_server(tmp_path):
+    """launch.js previews (TF_CONFIG, ClusterSpec, rendered command) equal core/launcher.py + Task.render."""
+    from tensorhive_fixed_amd.core import launcher
+
+    pl = [{"hostname": "a", "role": "chief", "gpus": [0]}, {"hostname": "a", "role": "worker", "gpus": [1]},
+          {"hostname": "b", "role": "worker", "gpus": [0]}, {"hostname": "b", "role": "ps", "gpus": []}]
+    out = _node_eval(tmp_path, r"""
+import { tf2Preview, tf1Preview, renderCommand, parseSegments, segmentsToText } from "@JS@/launch.js";
+const pl = %s;
+const segs = parseSegments("HIP_VISIBLE_DEVICES=0,1\nNCCL_DEBUG=WARN", "--nproc_per_node=2\n-m mod\n--flag");
+console.log(JSON.stringify({ tf2: tf2Preview(pl, 2222), tf1: tf1Preview(pl, 2222), segs,
+  cmd: renderCommand("torchrun", segs), back: segmentsToText(segs) }));
+""" % json.dumps(pl))
+    ref2 = launcher.tf2_tasks([(p["hostname"], p["role"], 0) for p in pl], 2222)
+    assert [x["TF_CONFIG"] for x in out["tf2"]] == [
+        json.dumps(json.loads(next(e["value"] for e in t["cmdsegments"]["envs"] if e["name"] == "TF_CONFIG")))
+        .replace(" ", "") for t in ref2]
+    ref1 = launcher.tf1_tasks(["b"], [("a", 0), ("a", 1), ("b", 0)], 2222)
+    flags = [" ".join(p["name"] + p["value"] for p in t["cmdsegments"]["params"]) for t in ref1]
+    assert [x["flags"] for x in out["tf1"]] == flags
+    assert out["segs"]["params"] == [{"name": "--nproc_per_node=", "value": "2"}, {"name": "-m", "value": "mod"},
+                                     {"name": "--flag", "value": ""}]
+    from tensorhive_fixed_amd.models.orm import Task
+    t = Task(command="torchrun", hostname="h")
+    assert out["cmd"] == t.render([(e["name"], e["value"]) for e in out["segs"]["envs"]],
+                                  [(p["name"], p["value"]) for p in out["segs"]["params"]])
+    assert out["back"]["params"].splitlines() == ["--nproc_per_node=2", "-m mod", "--flag"]
+
+
+def test_spa_schedule_and_calendar_math(tmp_path):
+    """time.js: UTC<->local schedule round trip, midnight-crossing windows, drag selection across
+    days and GPU columns, client-side restriction coverage, usage averages."""
+    out = _node_eval(tmp_path, """
+import * as T from "@JS@/time.js";
+const s = { scheduleDays: ["Monday", "Friday"], hourStart: "23:00", hourEnd: "02:00" };
+const loc = T.scheduleToLocal(s, 120), back = T.scheduleToUtc(loc, 120);
+const west = T.scheduleToLocal({ scheduleDays: ["Monday"], hourStart: "01:00", hourEnd: "05:00" }, -300);
+const days = [new Date("2026-01-05T00:00:00Z"), new Date("2026-01-06T00:00:00Z")];
+const sel = T.dragSelection({ day: 1, gpu: 2, slot: 3 }, { day: 0, gpu: 0, slot: 46 }, days, ["g0", "g1", "g2", "g3"], 30);
+const r = [{ isGlobal: false, resources: [{ id: "g1" }], startsAt: "2026-01-01T00:00:00Z", endsAt: null,
+             schedules: [{ scheduleDays: ["Monday"], hourStart: "08:00", hourEnd: "18:00" }] }];
+console.log(JSON.stringify({ loc, back, west, sel,
+  inWrap: [T.inSchedule(s, "2026-01-06T01:00:00Z"), T.inSchedule(s, "2026-01-06T03:00:00Z"), T.inSchedule(s, "2026-01-05T23:30:00Z")],
+  allow: [T.allowedWindow(r, "g1", "2026-01-05T09:00:00Z", "2026-01-05T12:00:00Z"),
+          T.allowedWindow(r, "g1", "2026-01-05T17:00:00Z", "2026-01-05T19:00:00Z"),
+          T.allowedWindow(r, "g2", "2026-01-05T09:00:00Z", "2026-01-05T10:00:00Z")],
+  lay: T.layoutDay([{ start: "2026-01-04T22:00:00Z", end: "2026-01-05T06:00:00Z" }], days[0]),
+  use: T.usageSummary([{ gpuUtilAvg: 80, memUtilAvg: 40 }, { gpuUtilAvg: 60, memUtilAvg: null }, { gpuUtilAvg: null }]),
+  valid: [T.validReservationRange("2026-01-05T00:00:00Z", "2026-01-05T00:20:00Z"), T.validReservationRange("2026-01-05T00:00:00Z", "2026-01-05T01:00:00Z")] }));
+""")
+    assert out["loc"]["hourStartLocal"] == "01:00" and out["loc"]["hourEndLocal"] == "04:00"
+    assert out["loc"]["scheduleDaysLocal"] == ["Tuesday", "Saturday"]
+    assert out["back"] == {"scheduleDays": ["Monday", "Friday"], "hourStart": "23:00", "hourEnd": "02:00"}
+    assert out["west"]["scheduleDaysLocal"] == ["Sunday"] and out["west"]["hourStartLocal"] == "20:00"
+    assert out["sel"] == {"start": "2026-01-05T23:00:00.000Z", "end": "2026-01-06T02:00:00.000Z", "gpus": ["g0", "g1", "g2"]}
+    assert out["inWrap"] == [True, False, True]
+    assert out["allow"] == [True, False, False]
+    assert out["lay"] == [{"r": {"start": "2026-01-04T22:00:00Z", "end": "2026-01-05T06:00:00Z"}, "top": 0, "height": 0.25}]
+    assert out["use"] == {"gpuUtilAvg": 70, "memUtilAvg": 40, "samples": 2}
+    assert out["valid"][0] and out["valid"][1] is None
 
 
 def test_cli_version_and_help():
