@@ -38,7 +38,9 @@ from .crud import CRUDModel
 log = logging.getLogger(__name__)
 
 _RESERVED_USERNAMES = {"root", "admin", "administrator", "api", "system", "null", "none", "daemon",
-                       "login", "logout", "signup", "register", "static", "www", "tensorhive"}
+                       "login", "logout", "signup", "register", "static", "www", "tensorhive",
+                       # insult words (the reference rejects them via the safe-usernames package)
+                       "jerk", "idiot", "moron", "stupid", "loser", "dumbass", "asshole", "bastard", "retard"}
 _USERNAME_RE = re.compile(r"^[A-Za-z0-9][A-Za-z0-9_.\-]*$")
 
 
