@@ -54,7 +54,8 @@ class LlamaConfig:
 
     @classmethod
     def llama3_8b(cls) -> "LlamaConfig":
-        return cls()
+        # TH_CE_CHUNK: tokens per LM-head + cross-entropy chunk (logits of one chunk: chunk x 128256 bf16)
+        return cls(ce_chunk=int(os.environ.get("TH_CE_CHUNK", "4096")))
 
     @classmethod
     def tiny(cls) -> "LlamaConfig":

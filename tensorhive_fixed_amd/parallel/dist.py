@@ -41,6 +41,12 @@ def apply_env_defaults() -> None:
         os.environ.setdefault(k, v)
 
 
+def forced_collectives() -> bool:
+    """TH_FORCE_COLLECTIVES=1: a one-rank run still creates the process group and issues every
+    collective (and the sharded optimizer), so the RCCL path can be tested on a one-GPU box."""
+    return os.environ.get("TH_FORCE_COLLECTIVES", "0") == "1"
+
+
 def init_distributed(device_type: str | None = None) -> DistInfo:
     """Initialise from the torchrun environment; single-process when WORLD_SIZE is absent."""
     apply_env_defaults()
@@ -57,7 +63,7 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
     else:
         device = torch.device("cpu")
     backend = None
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or forced_collectives()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = os.environ.get("TH_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")

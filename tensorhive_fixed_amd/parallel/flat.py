@@ -48,6 +48,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops.adamw import adamw_flat_, grad_sumsq_
+from .dist import forced_collectives
 
 _ALIGN = 64  # elements; keeps every view 128-byte aligned and every range a multiple of 8
 
@@ -89,6 +90,10 @@ class FlatParamStore:
         self.world = dist.get_world_size(process_group) if initialized else 1
         self.rank = dist.get_rank(process_group) if initialized else 0
         self.sharded = bool(shard)
+        # collectives run when there is more than one rank -- or, with TH_FORCE_COLLECTIVES=1, in a
+        # 1-rank group too, so the RCCL path (in-place reduce-scatter / all-gather on side streams)
+        # can be exercised on a one-GPU box (tests/gpu/test_ddp_gpu.py)
+        self.collectives = initialized and (self.world > 1 or forced_collectives())
         # decayed (matrices) first, then non-decayed vectors: two contiguous optimizer groups
         ordered = [e for e in params_in_backward_order if e[2]] + [e for e in params_in_backward_order if not e[2]]
         offs, self.buckets = self._layout([(p, d) for _, p, d in ordered], bucket_mb)
@@ -177,7 +182,7 @@ class FlatParamStore:
         self._ready_seen.add(key)
         b = self.param_bucket[key]
         b.pending -= 1
-        if b.pending == 0 and self._sync_now and self.world > 1:
+        if b.pending == 0 and self._sync_now and self.collectives:
             b.handle = self._launch_grad_collective(b)
 
     def finish_grad_sync(self) -> None:
@@ -185,7 +190,7 @@ class FlatParamStore:
         if len(self._ready_seen) != len(self.params):
             missing = [n for n, p in zip(self.names, self.params) if id(p) not in self._ready_seen]
             raise RuntimeError(f"no gradient delivered for: {missing[:5]}...")
-        if self.world == 1 or not self._sync_now:
+        if not self.collectives or not self._sync_now:
             return
         for b in self.buckets:
             if b.handle is None:
@@ -210,7 +215,7 @@ class FlatParamStore:
 
     def gather_bucket(self, index: int) -> None:
         """All-gather bucket ``index`` in place, asynchronously (after its slice was updated)."""
-        if not self.sharded or self.world == 1:
+        if not self.sharded or not self.collectives:
             return
         b = self.buckets[index]
         lo, hi = b.shard(self.rank, self.world)
@@ -324,7 +329,7 @@ class FlatAdamW:
                 grad_sumsq_(st.grad_buf[a:b], self.norm_sq, accumulate=i > 0)
             if not self.segments:
                 self.norm_sq.zero_()
-            if st.sharded and st.world > 1:
+            if st.sharded and st.collectives:
                 dist.all_reduce(self.norm_sq, op=dist.ReduceOp.SUM, group=st.pg)
         # forward order (last bucket first): in sharded mode each bucket's all-gather starts right after
         # its slice is updated, overlapping the remaining AdamW launches and then the next forward

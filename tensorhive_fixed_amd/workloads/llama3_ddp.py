@@ -23,7 +23,7 @@ import time
 import torch
 
 from ..models.llama3 import Llama, LlamaConfig
-from ..parallel.dist import DistInfo, barrier, init_distributed, max_over_ranks, shutdown
+from ..parallel.dist import DistInfo, barrier, forced_collectives, init_distributed, max_over_ranks, shutdown
 from ..parallel.flat import FlatAdamW, FlatParamStore
 
 
@@ -83,7 +83,7 @@ class Trainer:
         self.zero = default_zero(info.world) if zero is None else zero
         self.model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
         self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb,
-                                    shard=self.zero >= 1 and info.world > 1)
+                                    shard=self.zero >= 1 and (info.world > 1 or forced_collectives()))
         self.opt = FlatAdamW(self.store, lr=lr)
         if self.store.sharded or self.opt.overlap:
             self.model.param_gate = self.store.wait_params

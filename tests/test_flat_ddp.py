@@ -149,8 +149,11 @@ def _zero_rank_main(rank, world, port, out_dir, steps):
     shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_zero1_sharded_optimizer_matches_replicated(tmp_path, world):
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_zero1_sharded_optimizer_matches_replicated(tmp_path, world, monkeypatch):
+    """world 1 runs with TH_FORCE_COLLECTIVES=1: a one-rank group still issues every collective."""
+    if world == 1:
+        monkeypatch.setenv("TH_FORCE_COLLECTIVES", "1")
     steps = 3  # step 2+ runs its forward on all-gathered parameters
     mp.start_processes(_zero_rank_main, args=(world, _free_port(), str(tmp_path), steps), nprocs=world, join=True,
                        start_method="spawn")
