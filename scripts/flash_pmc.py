@@ -16,6 +16,6 @@ for _ in range(5):
     o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D, variant=None if var is None else int(var))
 do = torch.randn_like(o)
 for _ in range(3):
-    flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)
+    flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D, flags=int(os.environ.get("FA_BWD_FLAGS", "0")))
 torch.cuda.synchronize()
 print("done")

@@ -972,6 +972,231 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
   }
 }
 
+// ---------------------------------------------------- paired dK | dV kernel, one barrier per tile
+// Same roles and MFMA work as kc_body (DMA mode), rescheduled around ONE workgroup barrier per
+// 64-query tile instead of two.  The two-barrier schedule parks each role at every phase boundary
+// behind the other role's VALU (P = exp in phase 1 on the dV side, dS = P (dP - delta) in phase 2
+// on the dK side): SQ_WAIT_ANY 38 % of wave cycles, MFMA busy 36 % (profiles/r02_flash).
+//   * Q/dO tiles in a 3-deep LDS ring: tile t+1's DMA is issued right after the barrier of tile
+//     t-1, so the single barrier of tile t (vmcnt(0) + lgkmcnt(0) + s_barrier, placed between
+//     phase 1 and phase 2) both publishes P(t) and makes tile t+1 visible -- phase 1 of t+1 needs
+//     no barrier of its own;
+//   * P crosses between the pair as bf16 (the value the dV MFMA consumes anyway) through a
+//     double-buffered 4 KB-per-pair slot, because phase 1 of t+1 (writer) may overlap phase 2 of t
+//     (reader);
+//   * after barrier t: ring slot (t+2)%3 and P slot (t+1)&1 are free (their last readers ran phase
+//     2 of t-1, before phase 1 of t).
+// LDS: 3 x 33 KB tiles + 32 KB P = 130 KB (one workgroup per CU, as before).
+constexpr int KC3_PB = 4 * 4096;  // one P slot: 4 wave pairs x 4 KB (bf16)
+
+template <bool DK>
+__device__ __forceinline__ void kc3_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
+                                         const float* __restrict__ LSE, const float* __restrict__ Dl,
+                                         const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
+                                         char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
+                                         long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  const int k0 = kblk0 + 32 * w;
+  const int key = k0 + c32;
+  const ushort* fb = DK ? Vb : Kb;
+  bf16x8 kf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    kf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
+  f32x16 acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
+
+  const int nqt = (S + C_BQ - 1) / C_BQ;
+  const int qt0 = causal ? kblk0 / C_BQ : 0;
+  const int per_head = nqt - qt0;
+  const int total = G * per_head;
+  float lr = 0.f, dr = 0.f;
+  int lq = 0;
+  unsigned rc[4];
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto tile_at = [&](int i) { return smem + (i % 3) * KC_TILE; };
+  auto dma_tile = [&](int h_i, int t_i, int i) {
+    const int hq = hk * G + h_i;
+    const int qq0 = (qt0 + t_i) * C_BQ;
+    const ushort* base = DK ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
+    const long ldx = DK ? ld : ldo;
+    const unsigned img = lds0 + (i % 3) * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 4096;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
+      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
+    }
+  };
+  // lse / delta of one tile: raw loads into registers one tile before they are written to LDS
+  // (the write makes the compiler wait for them -- done BEFORE the next DMA issue, so that wait
+  // never covers a just-issued tile DMA it cannot see)
+  auto load_ld = [&](int h_i, int t_i) {
+    if (DK && tid < C_BQ) {
+      const int hq = hk * G + h_i;
+      lq = (qt0 + t_i) * C_BQ + tid;
+      const long st = ((long)b * Hq + hq) * S;
+      const int qc = min(lq, S - 1);
+      lr = LSE[st + qc];
+      dr = Dl[st + qc];
+    }
+  };
+  auto write_ld = [&](int i) {
+    if (DK && tid < C_BQ) {
+      float* l = reinterpret_cast<float*>(tile_at(i) + 2 * C_BQ * 256);
+      l[tid] = lq < S ? lr * LOG2E : INFINITY;  // rows past S: P = 0 exactly
+      l[C_BQ + tid] = lq < S ? dr : 0.f;
+    }
+  };
+  int dh = 0, dt = 0;  // (head, tile) of the next DMA
+  int lh = 0, lt = 0;  // (head, tile) of the lse / delta registers
+  auto adv = [&](int& hh, int& tt) {
+    if (++tt == per_head) { tt = 0; ++hh; }
+  };
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // K/V fragment loads retired (a wait the compiler sees)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) rc[u] = img_rc(wu * 4096 + u * 1024 + lane * 16);
+  // prologue: tiles 0 and 1 in flight, lse / delta of tile 2 in registers
+  for (int i = 0; i < 2 && i < total; ++i) {
+    load_ld(lh, lt);
+    write_ld(i);
+    adv(lh, lt);
+    dma_tile(dh, dt, i);
+    adv(dh, dt);
+  }
+  if (total > 2) load_ld(lh, lt);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  ushort4v* pslot = reinterpret_cast<ushort4v*>(smem + 3 * KC_TILE + w * 4096);
+  int cur_t = 0;
+  for (int it = 0; it < total; ++it) {
+    const char* cur = tile_at(it);
+    const char* qs = cur;
+    const char* gs = cur + C_BQ * 256;
+    const float* ls = reinterpret_cast<const float*>(cur + 2 * C_BQ * 256);
+    const float* ds = ls + C_BQ;
+    ushort4v* pb = pslot + (it & 1) * (KC3_PB / 8);
+    const int qbase = (qt0 + cur_t) * C_BQ;
+    if (++cur_t == per_head) cur_t = 0;
+    // phase 1: dK role dP = dO V^T, dV role S = Q K^T -> P (bf16 to the pair's P slot)
+    f32x16 c[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int q0 = qbase + 32 * kb;
+      c[kb] = f32x16(0.f);
+      if (causal && q0 + 31 < k0) continue;
+      const char* img = DK ? gs : qs;
+      bf16x8 xa[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) xa[s] = lds_row(img, 32 * kb + c32, 2 * s + h);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        bf16x8 xn = xa[s & 1];
+        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
+        __builtin_amdgcn_sched_barrier(0);
+        c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
+        __builtin_amdgcn_sched_barrier(0);
+        xa[s & 1] = xn;
+      }
+      if (!DK) {
+        const bool tile_mask = causal && q0 < k0 + 31;
+        const int mthr = tile_mask ? key - q0 - 4 * h : -0x7fffffff;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
+          ushort4v pw;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float p = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
+            const float pm = mthr > e + 8 * g ? 0.f : p;
+            pw[e] = f2bf(pm);
+            c[kb][4 * g + e] = bf2f(pw[e]);  // the dV MFMA and the dK side use the same rounded P
+          }
+          pb[(kb * 4 + g) * 64 + lane] = pw;
+        }
+      }
+    }
+    // the tile's one barrier: P(it) published; tile it+1 (DMA issued a tile ago) landed everywhere;
+    // every wave is past phase 2 of it-1, so ring slot (it+2)%3 and P slot (it+1)&1 are free
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (it + 2 < total) {
+      write_ld(it + 2);
+      adv(lh, lt);
+      dma_tile(dh, dt, it + 2);
+      adv(dh, dt);
+      if (it + 3 < total) load_ld(lh, lt);
+    }
+    // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int q0 = qbase + 32 * kb;
+      if (causal && q0 + 31 < k0) continue;
+      if (DK) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const ushort4v pw = pb[(kb * 4 + g) * 64 + lane];
+          const float4v dv4 = *reinterpret_cast<const float4v*>(ds + 32 * kb + 4 * h + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = bf2f(pw[e]) * (c[kb][4 * g + e] - dv4[e]);
+        }
+      }
+      const bf16x8 s0 = pack8(c[kb], 0), s1 = pack8(c[kb], 8);
+      const char* op = DK ? qs : gs;
+      bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        bf16x8 n0 = t0, n1 = t1;
+        if (d < 3) {
+          n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
+          n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc[d] = mfma(t0, s0, acc[d]);
+        acc[d] = mfma(t1, s1, acc[d]);
+        __builtin_amdgcn_sched_barrier(0);
+        t0 = n0;
+        t1 = n1;
+      }
+    }
+  }
+  if (key < S) {
+    ushort* orow = out + b * bs + (long)key * ld + (long)hk * HD;
+    const float f = DK ? scale : 1.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4v o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[d][4 * g + e] * f);
+        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = o;
+      }
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void fa_bwd_kc3_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  __shared__ __attribute__((aligned(1024))) char smem[3 * KC_TILE + 2 * KC3_PB];
+  const int nkb = (S + C_BK - 1) / C_BK;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = L / nkb, kb_i = L % nkb;
+  const int b = grp / Hkv, hk = grp % Hkv;
+  const int kblk = causal ? kb_i : nkb - 1 - kb_i;
+  const int G = Hq / Hkv;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+  if (threadIdx.x >= 256)
+    kc3_body<false>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+                    scale_log2, causal);
+  else
+    kc3_body<true>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+                   scale_log2, causal);
+}
+
 template <bool DMA>
 __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
@@ -1066,7 +1291,11 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernel)
   if (!(flags & 8)) {
     const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;
-    if (dq_dma && !(flags & 64))  // same 32-bit offset bound; bit5 or bit6: register staging here
+    if (dq_dma && (flags & 128))  // bit7: one barrier per tile (3-deep Q/dO ring, bf16 P exchange)
+      fa_bwd_kc3_kernel<<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                      (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
+                                                      B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+    else if (dq_dma && !(flags & 64))  // same 32-bit offset bound; bit5 or bit6: register staging here
       fa_bwd_kc_kernel<true><<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                            (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
                                                            B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
