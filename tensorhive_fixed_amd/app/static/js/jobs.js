@@ -46,6 +46,18 @@ export function jobsView(root, params) {
     const d = await call("GET", "/jobs" + qs({ userId: who === "all" ? undefined : who === "mine" ? S.me : +who })).catch(e => { errToast(e); return null; });
     if (!v.alive || !d) return;
     jobs = d.jobs || [];
+    // a job document carries no tasks (reference models/Job.py as_dict): mine come from one
+    // GET /tasks, another user's per job
+    const byJob = {};
+    if (who === "mine") {
+      const t = await call("GET", "/tasks" + qs({ syncAll: false })).catch(() => ({ tasks: [] }));
+      (t.tasks || []).forEach(x => (byJob[x.jobId] = byJob[x.jobId] || []).push(x));
+    } else {
+      await Promise.all(jobs.slice(0, 100).map(j => call("GET", "/tasks" + qs({ jobId: j.id, syncAll: false }))
+        .then(t => { byJob[j.id] = t.tasks || []; }).catch(() => null)));
+    }
+    if (!v.alive) return;
+    jobs.forEach(j => { j.tasks = byJob[j.id] || []; });
     const uname = id => (users.find(u => u.id === id) || {}).username || id;
     box.replaceChildren(table([
       { label: h("input", { type: "checkbox", onchange: e => { jobs.forEach(j => e.target.checked ? chosen.add(j.id) : chosen.delete(j.id)); load(); } }),
@@ -112,9 +124,11 @@ function jobDetailsView(root, id) {
   let job = null, editing = false, openLog = null;
 
   async function load() {
-    const d = await call("GET", `/jobs/${id}`).catch(e => { errToast(e); return null; });
+    const [d, t] = await Promise.all([call("GET", `/jobs/${id}`), call("GET", "/tasks" + qs({ jobId: id, syncAll: false }))])
+      .catch(e => { errToast(e); return [null, null]; });
     if (!v.alive || !d) return;
     job = d.job;
+    job.tasks = (t && t.tasks) || [];
     if (!editing) renderInfo();
     renderTasks();
   }
@@ -162,7 +176,7 @@ function jobDetailsView(root, id) {
       job.tasks || [], { empty: "no tasks: add one below" }),
       h("div", { class: "row" }, h("button", { class: "pri", onclick: () => taskDialog(job, null, false, load) }, "add task"),
         h("button", { onclick: () => launchDialog(job, load) }, "distributed launch"),
-        h("button", { onclick: () => adoptDialog(job, load) }, "add existing task"))));
+        h("button", { onclick: () => adoptDialog(job, load) }, "move a task here"))));
   }
 
   // log viewer: follows the file every 5 s while open; training curve from [th-train] lines
@@ -290,13 +304,14 @@ async function taskDialog(job, task, duplicate, reload) {
   }, "pri"]]);
 }
 
-// Tasks of the user that are not in any job (GET /tasks?jobId=null) can be added to this one
+// Move one of the user's tasks of another job into this one (GET /tasks?jobId=null lists the
+// tasks of all the caller's jobs, as the reference's FullCalendarInfo.vue used it)
 async function adoptDialog(job, reload) {
   const d = await call("GET", "/tasks" + qs({ jobId: null, syncAll: false })).catch(e => { errToast(e); return null; });
   if (!d) return;
   const tasks = (d.tasks || []).filter(t => t.jobId === null || t.jobId === undefined || t.jobId !== job.id);
   const sel = select(tasks.map(t => [t.id, `#${t.id} ${t.hostname}: ${t.fullCommand.slice(0, 60)}`]));
-  modal("Add an existing task", tasks.length ? field("task", sel) : h("p", { class: "mut" }, "no free tasks"),
+  modal("Move a task into this job", tasks.length ? field("task", sel) : h("p", { class: "mut" }, "no tasks in other jobs"),
     tasks.length ? [["Add", async () => {
       const ok = await attempt(() => call("PUT", `/jobs/${job.id}/tasks/${sel.value}`), "task added");
       if (!ok) return false;

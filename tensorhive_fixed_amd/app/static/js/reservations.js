@@ -247,7 +247,9 @@ export function reservationsView(root) {
     const d = await call("GET", "/jobs" + qs({ userId: S.me })).catch(() => ({ jobs: [] }));
     const free = await call("GET", "/tasks" + qs({ jobId: null, syncAll: false })).catch(() => ({ tasks: [] }));
     const jobs = (d.jobs || []).filter(j => j.status !== "running");
-    const sel = select(jobs.map(j => [j.id, `#${j.id} ${j.name} (${(j.tasks || []).length} task(s))`]));
+    const count = {};
+    (free.tasks || []).forEach(t => { count[t.jobId] = (count[t.jobId] || 0) + 1; });
+    const sel = select(jobs.map(j => [j.id, `#${j.id} ${j.name} (${count[j.id] || 0} task(s))`]));
     const sib = h("input", { type: "checkbox", checked: true });
     box.replaceChildren(h("h4", {}, "Run a job inside this reservation"),
       jobs.length ? h("div", { class: "row" }, sel, h("label", { title: "also use my other reservations of the same window on this node" }, sib, " + sibling GPUs"),
@@ -255,7 +257,7 @@ export function reservationsView(root) {
           await call("PUT", `/jobs/${sel.value}/reservation/${r.id}` + qs({ siblings: sib.checked }));
         }, "job attached: its tasks run on the reserved GPUs at the reservation start") }, "attach"))
         : h("p", { class: "mut" }, "no stopped jobs to attach"),
-      (free.tasks || []).length ? h("p", { class: "mut" }, `${free.tasks.length} task(s) of yours are not in a job`) : null);
+      h("p", { class: "mut" }, "the job's tasks get the reserved GPUs as HIP_VISIBLE_DEVICES and start / stop at the reservation window"));
   }
 
   // ---------------------------------------------------------------- my schedule

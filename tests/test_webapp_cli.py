@@ -1,6 +1,7 @@
 """Dashboard server, CLI entry points, doctor/benchmark harnesses (reference ``cli.py``,
 ``app/web/AppServer.py``)."""
 import json
+import os
 import re
 import shutil
 import subprocess
@@ -263,3 +264,59 @@ def test_doctor_reports_without_gpu(monkeypatch):
     checks = {n: (ok, d) for n, ok, d in doctor.run_checks()}
     assert "rocm" in checks and "torch (ROCm)" in checks
     assert json.dumps([list(c) for c in checks.items()])  # serialisable
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_spa_end_to_end_against_live_api(tmp_path):
+    """The dashboard modules run under node (tests/spa/dom.mjs: a minimal DOM + fetch over http)
+    against a real threaded API server with a file database: every view renders, and users /
+    schedules / groups are created through their dialogs, a drag over two GPU columns reserves
+    both, the reservation card edits it, a job gets a task, a duplicate and three TF2 tasks from the
+    launch editor, the router shows the account page, the password changes and logout revokes."""
+    import threading
+    from datetime import timedelta
+
+    from werkzeug.serving import make_server
+
+    from tensorhive_fixed_amd import benchmarks
+    from tensorhive_fixed_amd.api.app import create_app
+    from tensorhive_fixed_amd.core.daemon import Daemon
+    from tensorhive_fixed_amd.core.telemetry import StubBackend
+    from tensorhive_fixed_amd.models.orm import Restriction, Role, User
+    from tensorhive_fixed_amd.utils import dates
+
+    hosts = {"node-a": "fake"}
+    with benchmarks.sandbox(hosts, stub_gpus=4) as (cfg, _d):
+        stub = StubBackend(gpus_per_host=4)
+        daemon = Daemon(cfg, backends={h: stub for h in hosts}, init_key=False, test_ssh=False)
+        daemon.infrastructure.publish("node-a", stub.sample("node-a"))
+        app = create_app(daemon)
+        admin = User(username="spaadmin", password="admin password 1", email="a@example.org",
+                     roles=[Role(name="user"), Role(name="admin")])
+        admin.save()
+        user = User(username="spaalice", password="alice password 1", email="alice@example.org",
+                    roles=[Role(name="user")])
+        user.save()
+        r = Restriction(name="everything", starts_at=dates.utcnow() - timedelta(days=1), is_global=True)
+        r.save()
+        r.apply_to_user(user)
+        r.apply_to_user(admin)
+        app.test_client().get("/api/nodes/metrics", headers=benchmarks._headers(admin))  # registers the GPUs
+        srv = make_server("127.0.0.1", 0, app, threaded=True)
+        th = threading.Thread(target=srv.serve_forever, daemon=True)
+        th.start()
+        try:
+            scen = Path(__file__).resolve().parent / "spa" / "scenario.mjs"
+            p = subprocess.run(["node", str(scen), f"http://127.0.0.1:{srv.server_port}", "spaadmin",
+                                "admin password 1", "spaalice", "alice password 1"],
+                               capture_output=True, text=True, timeout=240, env={**os.environ, "TZ": "UTC"})
+        finally:
+            srv.shutdown()
+            daemon.shutdown()
+    assert p.returncode == 0, p.stderr[-3000:]
+    doc = json.loads(p.stdout.strip().splitlines()[-1])
+    (tmp_path / "spa_scenario.json").write_text(json.dumps(doc, indent=1))
+    bad = [s for s in doc["steps"] if not s["ok"]]
+    assert not doc["errors"], (doc["errors"][:3], [(s["name"], s["ok"], str(s.get("detail"))[:150]) for s in doc["steps"]])
+    assert not bad, bad
+    assert len(doc["steps"]) >= 23 and doc["requests"] > 60
