@@ -481,3 +481,31 @@ def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3) -> dict:
         if line.startswith("{"):
             return json.loads(line)
     raise RuntimeError(f"bench.py failed ({r.returncode}): {r.stderr[-2000:]}")
+
+
+def scaling(gpu_counts: list[int] | None = None, steps: int = 10, warmup: int = 3,
+            run=None, available: int | None = None) -> dict:
+    """Weak-scaling curve of the training payload on one node (N08 c): ``bench.py`` at each GPU
+    count (torchrun, one rank per GPU, RCCL), the per-N whole-job tokens/s and the efficiency
+    ``tokens_per_sec(N) / (N * tokens_per_sec(1))``.  Counts above the node's GPUs are skipped."""
+    if available is None:
+        import torch
+
+        available = torch.cuda.device_count()
+    counts = [n for n in (gpu_counts or [1, 2, 4, 8]) if 1 <= n <= max(available, 1)]
+    if 1 not in counts:
+        counts = [1] + counts
+    run = run or (lambda n: train_throughput(n, steps, warmup))
+    points = []
+    base = None
+    for n in counts:
+        doc = run(n)
+        v = float(doc["value"])
+        if n == 1:
+            base = v
+        points.append({"n_gpus": n, "tokens_per_sec": v, "ms_per_step": doc.get("ms_per_step"),
+                       "tokens_per_sec_per_gpu": round(v / n, 1),
+                       "efficiency": round(v / (n * base), 4) if base else None,
+                       "zero": (doc.get("config") or {}).get("zero")})
+    return {"metric": "llama3_8b_bf16_ddp_train_tokens_per_sec", "scaling": "weak", "points": points,
+            "skipped": [n for n in (gpu_counts or [1, 2, 4, 8]) if n not in counts]}

@@ -214,13 +214,13 @@ def doctor():
 
 
 @main.command()
-@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled", "multitenant"]))
+@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled", "multitenant", "scaling"]))
 @click.option("--requests", default=1000)
 @click.option("--gpus", default=1)
 @click.option("--pinned", is_flag=True, help="multitenant: reference-style pinned device pairs")
 def bench(what, requests, gpus, pinned):
     """Benchmarks of BASELINE.md: poll latency, queued-job launch latency, multi-tenant queue
-    wait / GPU utilisation, training tokens/s."""
+    wait / GPU utilisation, training tokens/s, and its 1/2/4/8-GPU weak-scaling curve."""
     from . import benchmarks
 
     if what == "multitenant":
@@ -231,6 +231,8 @@ def bench(what, requests, gpus, pinned):
         click.echo(json.dumps(benchmarks.launch_latency()))
     elif what == "scheduled":
         click.echo(json.dumps(benchmarks.scheduled_training(gpus)))
+    elif what == "scaling":  # 1, 2, 4, 8 GPUs (or up to --gpus), weak-scaling efficiency
+        click.echo(json.dumps(benchmarks.scaling([n for n in (1, 2, 4, 8) if n <= max(gpus, 8)])))
     else:
         click.echo(json.dumps(benchmarks.train_throughput(gpus)))
 

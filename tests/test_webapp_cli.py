@@ -320,3 +320,15 @@ def test_spa_end_to_end_against_live_api(tmp_path):
     assert not doc["errors"], (doc["errors"][:3], [(s["name"], s["ok"], str(s.get("detail"))[:150]) for s in doc["steps"]])
     assert not bad, bad
     assert len(doc["steps"]) >= 23 and doc["requests"] > 60
+
+
+def test_scaling_harness_efficiency_and_skips():
+    from tensorhive_fixed_amd import benchmarks
+
+    fake = {1: 24700.0, 2: 49000.0, 4: 97500.0, 8: 193000.0}
+    out = benchmarks.scaling([1, 2, 4, 8], available=4,
+                             run=lambda n: {"value": fake[n], "ms_per_step": 1000.0, "config": {"zero": int(n > 1)}})
+    assert [p["n_gpus"] for p in out["points"]] == [1, 2, 4] and out["skipped"] == [8]
+    eff = {p["n_gpus"]: p["efficiency"] for p in out["points"]}
+    assert eff[1] == 1.0 and abs(eff[2] - 49000 / 49400) < 1e-4 and abs(eff[4] - 97500 / 98800) < 1e-4
+    assert out["points"][2]["tokens_per_sec_per_gpu"] == 24375.0 and out["points"][1]["zero"] == 1
