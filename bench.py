@@ -70,7 +70,7 @@ def main() -> int:
     from tensorhive_fixed_amd.models.llama3 import LlamaConfig
     from tensorhive_fixed_amd.ops import _lib
     from tensorhive_fixed_amd.ops.attention import attention_backend
-    from tensorhive_fixed_amd.parallel.dist import init_distributed, shutdown
+    from tensorhive_fixed_amd.parallel.dist import barrier, init_distributed, shutdown
     from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer, run_timed
 
     if torch.cuda.is_available():
@@ -118,6 +118,7 @@ def main() -> int:
     if info.is_main:
         line["daemon"] = daemon_poll_latency() if args.daemon_bench else None
         print(json.dumps(line), flush=True)
+    barrier(info)  # the other ranks keep their RCCL communicator until rank 0's daemon bench is done
     shutdown()
     return 0
 
