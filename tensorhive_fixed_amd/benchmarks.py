@@ -280,10 +280,12 @@ def launch_latency(trials: int = 5, command: str = "echo started; sleep 2") -> d
 
 
 def scheduled_training(gpus: int = 1, steps: int = 10, warmup: int = 2, micro_batch: int = 8,
-                       model: str = "llama3-8b", timeout_s: float = 900.0) -> dict:
+                       model: str = "llama3-8b", timeout_s: float = 900.0, auto: bool = True) -> dict:
     """BASELINE config 3/4: the Llama-3 DDP payload launched BY THE JOB QUEUE -- torchrun template,
-    HIP_VISIBLE_DEVICES from the GPUs' HIP indices, real amdsmi telemetry for the free-GPU check --
-    and its tokens/s read back from the task log (``[th-train]`` lines)."""
+    real amdsmi telemetry for the free-GPU check -- and its tokens/s read back from the task log
+    (``[th-train]`` lines).  ``auto``: the task asks for ``HIP_VISIBLE_DEVICES=auto:N`` and the
+    allocator picks the devices at launch (gang placement, ``core/allocation.py``); otherwise the
+    first N HIP indices are pinned."""
     import re
 
     from .core import task_nursery
@@ -310,7 +312,7 @@ def scheduled_training(gpus: int = 1, steps: int = 10, warmup: int = 2, micro_ba
         r = Restriction(name="all", starts_at=dates.utcnow(), is_global=True)
         r.save()
         r.apply_to_user(u)
-        form = torchrun_task("localhost", list(range(gpus)), "127.0.0.1", 29533,
+        form = torchrun_task("localhost", gpus if auto else list(range(gpus)), "127.0.0.1", 29533,
                              script_args=[("--steps", str(steps)), ("--warmup", str(warmup)),
                                           ("--micro-batch", str(micro_batch)), ("--model", model)])
         job = Job(name="llama3-ddp", description="scheduled training", user_id=u.id)
@@ -336,7 +338,10 @@ def scheduled_training(gpus: int = 1, steps: int = 10, warmup: int = 2, micro_ba
         finally:
             daemon.shutdown()
         steady = rates[1:] or rates
+        launched = task_ctl.Task.get(tid).as_dict()
         return {"metric": "scheduled_llama3_ddp_tokens_per_sec", "gpus": gpus, "micro_batch": micro_batch,
+                "placement": "auto" if auto else "pinned", "allocated_gpus": launched.get("allocatedGpus"),
+                "full_command": launched.get("fullCommand"),
                 "steps_logged": len(rates), "tokens_per_sec": round(statistics.fmean(steady), 1) if steady else None,
                 "completed": done, "wall_s": round(time.time() - t0, 1), "log_tail": lines[-3:]}
 
