@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 from pathlib import Path
 
@@ -34,7 +35,15 @@ class _ServerThread(threading.Thread):
         self.srv.shutdown()
 
 
+def quiet_access_log() -> None:
+    """werkzeug logs every request at INFO: four lines a second per open dashboard at the 0.25 s
+    poll, and ~0.1 ms of each poll.  Kept only with TENSORHIVE_ACCESS_LOG=1."""
+    if os.environ.get("TENSORHIVE_ACCESS_LOG", "0") != "1":
+        logging.getLogger("werkzeug").setLevel(logging.WARNING)
+
+
 def serve_wsgi(app, host: str, port: int, name: str = "wsgi") -> _ServerThread:
+    quiet_access_log()
     t = _ServerThread(app, host, port, name)
     t.start()
     return t

@@ -173,6 +173,9 @@ def poll_latency(requests: int = 1000, nodes: int = 8, gpus: int = 8, warmup: in
         # the user's view really is filtered: half of each node's GPUs
         seen = client.get("/api/nodes/metrics", headers=_headers(user)).get_json()
         visible = sum(len(v.get("GPU") or {}) for v in seen.values())
+        from .app.server import quiet_access_log
+
+        quiet_access_log()  # as the daemon's own server (app/server.py serve_wsgi)
         srv = make_server("127.0.0.1", 0, app, threaded=True)
         th = threading.Thread(target=srv.serve_forever, daemon=True)
         th.start()

@@ -8,16 +8,58 @@ read path).  Non-admins see only GPUs their restrictions allow.  Responses carry
 """
 from __future__ import annotations
 
+import datetime
 import threading
 
 from flask import Response
+from sqlalchemy import event
+from sqlalchemy.orm import Session
 
+from .. import database
 from ..api.app import daemon
 from ..database import db_session
-from ..models.orm import Resource, User
+from ..models.orm import Group, Resource, Restriction, RestrictionAssignee, User
+from ..utils import dates
 from ._common import M, is_admin, me
 
 _reg_lock = threading.Lock()
+
+# ------------------------------------------------------------------ permitted-GPU cache
+# A non-admin poll needs the set of GPUs the caller's restrictions cover: 4-6 queries (user,
+# restrictions, groups, their restrictions, resources), most of a restricted user's poll time.
+# The set is cached per (database, user) and dropped when (a) any flush touches a user, group,
+# restriction or resource (their association collections mark the owners dirty), or (b) one of
+# the user's restrictions starts or ends -- the set changes with the clock, without a write.
+_perm_epoch = [0]
+_perm_cache: dict = {}
+_perm_lock = threading.Lock()
+_PERM_TYPES = (User, Group, Restriction, RestrictionAssignee, Resource)
+
+
+@event.listens_for(Session, "after_flush")
+def _perm_invalidate(session, _ctx):
+    if any(isinstance(o, _PERM_TYPES) for o in (*session.new, *session.dirty, *session.deleted)):
+        with _perm_lock:
+            _perm_epoch[0] += 1
+            _perm_cache.clear()
+
+
+def allowed_gpus_cached(user_id: int) -> set[str] | None:
+    key = (id(database.engine()), user_id)
+    now = dates.utcnow()
+    with _perm_lock:
+        epoch = _perm_epoch[0]
+        hit = _perm_cache.get(key)
+    if hit is not None and hit[0] == epoch and now < hit[2]:
+        return hit[1]
+    user = User.get(user_id)
+    allowed = user.allowed_gpu_uuids()
+    bounds = [t for r in user.get_restrictions(include_expired=True, include_group=True)
+              for t in (r.starts_at, r.ends_at) if t is not None and t > now]
+    with _perm_lock:
+        if _perm_epoch[0] == epoch:  # nothing changed while we read
+            _perm_cache[key] = (epoch, allowed, min(bounds, default=datetime.datetime.max))
+    return allowed
 
 
 def _snapshot():
@@ -71,7 +113,7 @@ def filtered_view(data: dict, allowed: set[str] | None) -> dict:
 
 
 def _allowed() -> set[str] | None:
-    return None if is_admin() else User.get(me()).allowed_gpu_uuids()
+    return None if is_admin() else allowed_gpus_cached(me())
 
 
 def get_infrastructure() -> dict:

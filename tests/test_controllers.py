@@ -8,6 +8,7 @@ import pytest
 
 from tensorhive_fixed_amd.models.orm import (Group, Job, Reservation, Resource, Restriction, RestrictionSchedule,
                                              Task, User)
+from tensorhive_fixed_amd.database import db_session
 from tests.helpers import api
 
 UTC = datetime.datetime.utcnow
@@ -709,3 +710,45 @@ def test_internal_metrics_admin_only(as_user, as_admin):
     assert st == 403
     st, body = as_admin("get", "/metrics/internal")
     assert st == 200 and "api" in body
+
+
+def test_restricted_poll_cache_follows_writes_and_the_clock(client, new_user, new_admin, auth_headers, tables):
+    """/nodes/metrics for a non-admin caches the permitted-GPU set (controllers/nodes.py); every
+    permission write and every restriction start / end must show on the next poll."""
+    import time
+
+    hu, ha = auth_headers(new_user), auth_headers(new_admin)
+
+    def visible():
+        # the in-process client shares the fixtures' session (expire_on_commit=False); a served
+        # request starts from a fresh one
+        db_session.expire_all()
+        st, body = api(client, "get", "/nodes/metrics", hu)
+        assert st == 200
+        return {u for h in body.values() for u in (h.get("GPU") or {})}
+
+    api(client, "get", "/nodes/metrics", ha)  # registers the simulated GPUs as resources
+    uuids = sorted(r.id for r in Resource.all())
+    assert visible() == set()
+    r = Restriction(name="one gpu", starts_at=UTC() - timedelta(hours=1), is_global=False)
+    r.save()
+    r.apply_to_user(new_user)
+    r.apply_to_resource(Resource.get(uuids[0]))
+    assert visible() == {uuids[0]}
+    assert visible() == {uuids[0]}  # served from the cache
+    st, _ = api(client, "put", f"/restrictions/{r.id}/resources/{uuids[1]}", ha)
+    assert st == 200 and visible() == {uuids[0], uuids[1]}
+    g = Group(name="gpu-club")
+    g.save()
+    r2 = Restriction(name="club", starts_at=UTC() - timedelta(hours=1), ends_at=UTC() + timedelta(seconds=2),
+                     is_global=False)
+    r2.save()
+    r2.apply_to_group(g)
+    r2.apply_to_resource(Resource.get(uuids[2]))
+    assert visible() == {uuids[0], uuids[1]}
+    st, _ = api(client, "put", f"/groups/{g.id}/users/{new_user.id}", ha)
+    assert st == 200 and visible() == {uuids[0], uuids[1], uuids[2]}
+    time.sleep(2.2)  # r2 expires: no write happens, the cache entry's validity ends with it
+    assert visible() == {uuids[0], uuids[1]}
+    st, _ = api(client, "delete", f"/restrictions/{r.id}", ha)
+    assert st == 200 and visible() == set()
