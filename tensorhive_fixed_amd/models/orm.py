@@ -21,12 +21,14 @@ import datetime
 import enum
 import logging
 import re
+import threading
 from datetime import timedelta
 
 from sqlalchemy import (Boolean, Column, DateTime, Enum, ForeignKey, Integer, String, Text, Time, UniqueConstraint,
                         and_, or_)
 from sqlalchemy.exc import MultipleResultsFound, NoResultFound
-from sqlalchemy.orm import relationship, validates
+from sqlalchemy import event
+from sqlalchemy.orm import Session, relationship, validates
 
 from ..database import Base, db_session
 from ..utils import dates
@@ -122,9 +124,35 @@ class RevokedToken(CRUDModel, Base):
     id = Column(Integer, primary_key=True, autoincrement=True)
     jti = Column(String(120), unique=True, nullable=False)
 
+    # jtis already found absent from the table (per database): every authenticated request checks
+    # its token, and revocations only ever ADD rows, so a "not revoked" answer stays true until the
+    # next revocation -- which clears the set (after_flush listener below)
+    _absent: dict = {}
+    _absent_lock = threading.Lock()
+
     @classmethod
     def is_jti_blacklisted(cls, jti: str) -> bool:
-        return db_session.query(cls).filter_by(jti=jti).first() is not None
+        from .. import database
+
+        key = id(database.engine())
+        with cls._absent_lock:
+            if jti in cls._absent.get(key, ()):
+                return False
+        revoked = db_session.query(cls.id).filter_by(jti=jti).first() is not None
+        if not revoked:
+            with cls._absent_lock:
+                known = cls._absent.setdefault(key, set())
+                if len(known) > 100_000:
+                    known.clear()
+                known.add(jti)
+        return revoked
+
+
+@event.listens_for(Session, "after_flush")
+def _revocation_invalidates(session, _ctx):
+    if any(isinstance(o, RevokedToken) for o in session.new):
+        with RevokedToken._absent_lock:
+            RevokedToken._absent.clear()
 
 
 class User(CRUDModel, RestrictionAssignee, Base):

@@ -752,3 +752,12 @@ def test_restricted_poll_cache_follows_writes_and_the_clock(client, new_user, ne
     assert visible() == {uuids[0], uuids[1]}
     st, _ = api(client, "delete", f"/restrictions/{r.id}", ha)
     assert st == 200 and visible() == set()
+
+
+def test_revocation_visible_through_the_token_cache(client, new_user, auth_headers):
+    """RevokedToken caches 'not revoked' answers; a logout must still take effect immediately."""
+    h = auth_headers(new_user)
+    for _ in range(3):  # the jti is now cached as not revoked
+        assert api(client, "get", "/users", h)[0] == 200
+    assert api(client, "delete", "/user/logout", h)[0] == 200
+    assert api(client, "get", "/users", h)[0] == 401
