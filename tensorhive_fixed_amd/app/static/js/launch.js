@@ -4,13 +4,21 @@
 // tests/test_webapp_cli.py runs them under node against the Python implementations.
 "use strict";
 
+// One shell word per value, as the server renders it (models/orm.py _shell_value): values the
+// shell would split or strip (TF_CONFIG JSON, spaces, quotes, operators) are single-quoted.
+const SHELL_SPECIAL = /[\s"'{}\[\];&|<>()\\*?!#`]/;
+export function shellValue(v) {
+  v = v === undefined || v === null ? "" : String(v);
+  return SHELL_SPECIAL.test(v) ? "'" + v.replace(/'/g, "'\\''") + "'" : v;
+}
+
 // ENV=v ... command param value ...; a parameter whose name ends with "=" (or " ") is joined
 // without a separator, a parameter with an empty value is the bare name.
 export function renderCommand(command, segs) {
-  const parts = (segs.envs || []).map(e => `${e.name}=${e.value === undefined || e.value === null ? "" : e.value}`);
+  const parts = (segs.envs || []).map(e => `${e.name}=${shellValue(e.value)}`);
   parts.push(command);
   for (const p of segs.params || []) {
-    const v = p.value === undefined || p.value === null ? "" : String(p.value);
+    const v = shellValue(p.value);
     if (v === "") parts.push(p.name);
     else if (p.name.endsWith("=") || p.name.endsWith(" ")) parts.push(p.name + v);
     else parts.push(`${p.name} ${v}`);

@@ -50,6 +50,15 @@ def _utcnow():
     return dates.utcnow()
 
 
+_SHELL_SPECIAL = re.compile(r"""[\s"'{}\[\];&|<>()\\*?!#`]""")
+
+
+def _shell_value(v) -> str:
+    """A command-segment value as one shell word (see Task.render)."""
+    v = "" if v is None else str(v)
+    return "'" + v.replace("'", "'\\''") + "'" if _SHELL_SPECIAL.search(v) else v
+
+
 # ------------------------------------------------------------------------------------ users
 def _refresh_view(obj, attr: str) -> None:
     """The reverse side of a many-to-many is ``viewonly``: reload it after the owning side changed."""
@@ -861,10 +870,15 @@ class Task(CRUDModel, Base):
 
     def render(self, envs, params) -> str:
         """``ENV=v ... command param value ...`` from explicit segment lists (the launch path
-        substitutes allocated devices before rendering, see ``core/allocation.py``)."""
-        parts = [f"{n}={v}" for n, v in envs]
+        substitutes allocated devices before rendering, see ``core/allocation.py``).
+
+        The line runs under ``bash -lc``: a value the shell would split or strip -- a TF_CONFIG
+        JSON document, anything with spaces, quotes, braces or shell operators -- is single-quoted;
+        plain values stay as typed, so ``$HOME`` or ``~`` in them still expand."""
+        parts = [f"{n}={_shell_value(v)}" for n, v in envs]
         parts.append(self.command)
         for n, v in params:
+            v = _shell_value(v)
             if v == "":
                 parts.append(n)
             elif n.endswith("=") or n.endswith(" "):

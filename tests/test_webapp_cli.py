@@ -125,7 +125,7 @@ def test_spa_launch_previews_match_server(tmp_path):
     out = _node_eval(tmp_path, r"""
 import { tf2Preview, tf1Preview, renderCommand, parseSegments, segmentsToText } from "@JS@/launch.js";
 const pl = %s;
-const segs = parseSegments("HIP_VISIBLE_DEVICES=0,1\nNCCL_DEBUG=WARN", "--nproc_per_node=2\n-m mod\n--flag");
+const segs = parseSegments("HIP_VISIBLE_DEVICES=0,1\nNCCL_DEBUG=WARN\nTF_CONFIG={\"task\":{\"type\":\"chief\"}}", "--nproc_per_node=2\n-m mod\n--flag\n--msg it's done");
 console.log(JSON.stringify({ tf2: tf2Preview(pl, 2222), tf1: tf1Preview(pl, 2222), segs,
   cmd: renderCommand("torchrun", segs), back: segmentsToText(segs) }));
 """ % json.dumps(pl))
@@ -137,12 +137,13 @@ console.log(JSON.stringify({ tf2: tf2Preview(pl, 2222), tf1: tf1Preview(pl, 2222
     flags = [" ".join(p["name"] + p["value"] for p in t["cmdsegments"]["params"]) for t in ref1]
     assert [x["flags"] for x in out["tf1"]] == flags
     assert out["segs"]["params"] == [{"name": "--nproc_per_node=", "value": "2"}, {"name": "-m", "value": "mod"},
-                                     {"name": "--flag", "value": ""}]
+                                     {"name": "--flag", "value": ""}, {"name": "--msg", "value": "it's done"}]
+    assert "TF_CONFIG='{\"task\":{\"type\":\"chief\"}}'" in out["cmd"] and "--msg 'it'\\''s done'" in out["cmd"]
     from tensorhive_fixed_amd.models.orm import Task
     t = Task(command="torchrun", hostname="h")
     assert out["cmd"] == t.render([(e["name"], e["value"]) for e in out["segs"]["envs"]],
                                   [(p["name"], p["value"]) for p in out["segs"]["params"]])
-    assert out["back"]["params"].splitlines() == ["--nproc_per_node=2", "-m mod", "--flag"]
+    assert out["back"]["params"].splitlines() == ["--nproc_per_node=2", "-m mod", "--flag", "--msg it's done"]
 
 
 def test_spa_schedule_and_calendar_math(tmp_path):
