@@ -1,0 +1,193 @@
+// K-contiguous ("NT") GEMM for gfx950 (MI355X), the layout of the forward and input-gradient
+// products of every Llama linear layer:
+//
+//     C[M][N] (+)= sum_k A[M][k] * B[N][k]        (y = x W^T;  dX = dY (W^T)^T on a W^T copy)
+//
+// Same machine as the TN weight-gradient kernel (gemm_tn.hip, ping-pong v2), with the operand
+// path of the K-contiguous layout:
+//   * tile 256 x 256, k-tiles of 32 in a 4-stage LDS ring (4 x 32 KB); 8 waves as 2 (M) x 4 (N),
+//     wave tile 128 x 64, v_mfma_f32_32x32x16_bf16, 128 f32 accumulators per lane;
+//   * LDS-DMA (global_load_lds_dwordx4, inline asm, scalar base + one constant lane offset) stages
+//     16 rows x 64 B per wave-instruction; 16-B chunk c of row r lands in slot c ^ ((r >> 2) & 3),
+//     applied on the global source because the DMA writes lane-linearly;
+//   * an MFMA operand is ONE ds_read_b128 of a row (8 consecutive k), conflict-free under that
+//     swizzle: a 16-lane group reads 16 rows = (r & 3) 64-B quarters x ((r >> 2) & 3) slots;
+//   * ping-pong wave groups (G0 = waves 0-3, rows 0-127; G1 = waves 4-7, rows 128-255): one group
+//     gathers its fragments of k-tile t and issues its operand's DMA two k-tiles ahead while the
+//     other runs its 16 MFMAs, one barrier per slot, counted vmcnt (never 0 in the loop);
+//   * XCD-aware grouped tile order (bands of 8 tile rows per XCD).
+#include "th_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+#define LDS_AS __attribute__((address_space(3)))
+
+namespace {
+constexpr int TM = 256, TN = 256, TK = 32;
+constexpr int NTHR = 512;
+constexpr int ROWB = TK * 2;         // 64 B per staged row
+constexpr int OPB = TM * ROWB;       // 16 KB per operand image
+constexpr int STAGEB = 2 * OPB;      // A + B
+constexpr int NSTAGE = 4;
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lds_b128(const char LDS_AS* p) { return *reinterpret_cast<const bf16x8 LDS_AS*>(p); }
+
+// Rows [row0, row0+256) x k [k0, k0+32) of a row-major [rows][ld] operand into one 16 KB image:
+// 16 wave-instructions of 16 rows, 4 per wave of the staging group.  `loff` = the lane's constant
+// byte offset (row (lane>>2), swizzled chunk) from the instruction's scalar base.
+__device__ __forceinline__ void stage_nt(const ushort* __restrict__ g, unsigned loff, long ld, long row0, long k0,
+                                         unsigned img, int w4) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = i * 4 + w4;
+    glds16(g + (row0 + 16 * u) * ld + k0, loff, img + u * 1024);
+  }
+}
+
+__device__ __forceinline__ unsigned lane_off_nt(long ld, int lane) {
+  const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
+  return (unsigned)(2 * ((long)(lane >> 2) * ld + 8 * chunk));
+}
+
+// vmcnt(4 * n), n in 0..1 (immediate operand)
+__device__ __forceinline__ void wait_dma_barrier(int n) {
+  if (n >= 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+}
+}  // namespace
+
+template <bool BETA>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restrict__ A, long lda,
+                                                         const ushort* __restrict__ B, long ldb,
+                                                         ushort* __restrict__ C, long ldc, int M, int N, int K) {
+  constexpr int AHEAD = 2;
+  __shared__ __attribute__((aligned(1024))) char smem_raw[NSTAGE * STAGEB];
+  char LDS_AS* smem = (char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = L / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = L % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3, w4 = w & 3;
+  const bool g1 = w >= 4;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int nt = K / TK;
+
+  const int i32 = lane & 31, h = lane >> 5;
+  int ch[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) ch[ks] = ((2 * ks + h) ^ ((i32 >> 2) & 3)) * 16;
+  int a_row[4], b_row[2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) a_row[mb] = (wm * 128 + 32 * mb + i32) * ROWB;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) b_row[nb] = (wn * 64 + 32 * nb + i32) * ROWB;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
+
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  const unsigned la = lane_off_nt(lda, lane), lb = lane_off_nt(ldb, lane);
+#pragma unroll
+  for (int j = 0; j < AHEAD; ++j) {
+    if (j < nt) {
+      if (!g1) stage_nt(A, la, lda, m0, (long)j * TK, lds0 + j * STAGEB, w4);
+      else stage_nt(B, lb, ldb, n0, (long)j * TK, lds0 + j * STAGEB + OPB, w4);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (g1) asm volatile("s_barrier" ::: "memory");  // G1 enters one slot late
+
+  bf16x8 af[4][2], bf[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
+    // ---- gather slot (+ this group's operand DMA two k-tiles ahead)
+    if (t + AHEAD < nt) {
+      const unsigned st = lds0 + ((t + AHEAD) & (NSTAGE - 1)) * STAGEB;
+      if (!g1) stage_nt(A, la, lda, m0, (long)(t + AHEAD) * TK, st, w4);
+      else stage_nt(B, lb, ldb, n0, (long)(t + AHEAD) * TK, st + OPB, w4);
+    }
+    const char LDS_AS* sa = smem + (t & (NSTAGE - 1)) * STAGEB;
+    const char LDS_AS* sb = sa + OPB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) af[mb][ks] = lds_b128(sa + a_row[mb] + ch[ks]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = lds_b128(sb + b_row[nb] + ch[ks]);
+    }
+    if (g1) {  // G1's B image of k-tile t+1 lands before G0 gathers it (next slot)
+      wait_dma_barrier(younger);
+    } else {
+      asm volatile("s_barrier" ::: "memory");
+    }
+    // ---- compute slot
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!g1) {  // G0's A image of k-tile t+1 landed before the barrier that opens its gather
+      wait_dma_barrier(younger);
+    } else {
+      asm volatile("s_barrier" ::: "memory");
+    }
+  }
+  if (!g1) asm volatile("s_barrier" ::: "memory");
+
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const long n = n0 + wn * 64 + 32 * nb + i32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v = acc[mb][nb][r];
+        if (BETA) v += bf2f(C[m * ldc + n]);
+        C[m * ldc + n] = f2bf(v);
+      }
+    }
+}
+
+// C[M][N] (+)= A[M][K] B[N][K]^T (row strides lda, ldb, ldc in elements).  -1: shape not tiled.
+extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                          int beta, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK) return -1;
+  if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -1;
+  // the lane offset and the per-instruction scalar bases stay within 32-bit byte offsets per row block
+  if ((long)16 * lda * 2 >= (1L << 31) || (long)16 * ldb * 2 >= (1L << 31)) return -1;
+  const unsigned grid = (unsigned)((long)(M / TM) * (N / TN));
+  if (beta)
+    gemm_nt_kernel<true><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
+  else
+    gemm_nt_kernel<false><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
+  TH_CHECK_LAUNCH();
+}

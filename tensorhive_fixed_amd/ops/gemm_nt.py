@@ -1,0 +1,33 @@
+"""K-contiguous GEMM ``C (+)= A·Bᵀ`` (``csrc/gemm_nt.hip``): the forward ``x Wᵀ`` and input-gradient
+``dY (Wᵀ)ᵀ`` form of every Llama linear layer, on the gfx950 machinery of the TN weight-grad
+kernel.  Shapes it does not tile fall back to ``torch.mm``."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_TILE, _TK = 256, 32
+
+
+def supported(m: int, n: int, k: int) -> bool:
+    return m % _TILE == 0 and n % _TILE == 0 and k % _TK == 0
+
+
+def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation)."""
+    M, K = a.shape
+    N, K2 = b.shape
+    if K2 != K or tuple(out.shape) != (M, N):
+        raise ValueError(f"gemm_nt_: shapes {tuple(a.shape)}, {tuple(b.shape)} -> {tuple(out.shape)}")
+    ok = (a.is_cuda and a.dtype == b.dtype == out.dtype == torch.bfloat16 and supported(M, N, K)
+          and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1)
+    if not ok:
+        if accumulate:
+            out.addmm_(a, b.t())
+        else:
+            torch.mm(a, b.t(), out=out)
+        return out
+    _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
+              M, N, K, int(accumulate), _lib.stream_ptr(a.device))
+    return out
