@@ -39,6 +39,10 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         gemm_nt_(a, b, c)
         ref = a.float() @ b.float().t()
+        c16 = torch.empty_like(c)
+        gemm_nt_(a, b, c16, mfma16=True)
+        rel16 = ((c16.float() - ref).norm() / ref.norm()).item()
+        assert rel16 < 1e-2, rel16
         rel = ((c.float() - ref).norm() / ref.norm()).item()
         c0 = c.clone()
         gemm_nt_(a, b, c, accumulate=True)
@@ -53,14 +57,16 @@ def main():
         gemm_nt_(a, b, c)
         torch.mm(a, b.t(), out=c2)
         diff = ((c.float() - c2.float()).norm() / c2.float().norm()).item()
-        res = {"nt": [], "hipblaslt": []}
+        res = {"nt": [], "nt16": [], "hipblaslt": []}
         for _ in range(3):
             res["nt"].append(timed(lambda: gemm_nt_(a, b, c)))
+            res["nt16"].append(timed(lambda: gemm_nt_(a, b, c, mfma16=True)))
             res["hipblaslt"].append(timed(lambda: torch.mm(a, b.t(), out=c2)))
         fl = 2.0 * M * N * K
-        nt, hb = min(res["nt"]), min(res["hipblaslt"])
+        nt, nt16, hb = min(res["nt"]), min(res["nt16"]), min(res["hipblaslt"])
         print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "nt_ms": round(nt, 4), "hipblaslt_ms": round(hb, 4),
-                          "nt_tflops": round(fl / nt / 1e9), "hipblaslt_tflops": round(fl / hb / 1e9),
+                          "nt_tflops": round(fl / nt / 1e9), "nt16_tflops": round(fl / nt16 / 1e9),
+                          "hipblaslt_tflops": round(fl / hb / 1e9),
                           "speedup": round(hb / nt, 3), "rel_diff_vs_hipblaslt": diff}), flush=True)
         del a, b, c, c2
     return 0

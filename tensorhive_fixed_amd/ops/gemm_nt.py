@@ -14,7 +14,8 @@ def supported(m: int, n: int, k: int) -> bool:
     return m % _TILE == 0 and n % _TILE == 0 and k % _TK == 0
 
 
-def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+             mfma16: bool = False) -> torch.Tensor:
     """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation)."""
     M, K = a.shape
     N, K2 = b.shape
@@ -29,5 +30,5 @@ def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
             torch.mm(a, b.t(), out=out)
         return out
     _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), int(mfma16), _lib.stream_ptr(a.device))
     return out
