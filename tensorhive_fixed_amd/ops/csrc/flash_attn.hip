@@ -515,13 +515,20 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         pacc = mfma(lds_row(vs, 32 * kb + c32, 2 * s + h), gf[s], pacc);
       }
 #endif
-      // tile-relative last visible key of this lane's query (INT_MAX: the tile needs no mask)
-      const int kmax = need_mask ? (causal ? min(q, S - 1) : S - 1) - kbase - 32 * kb - 4 * h : 0x7fffffff;
+      // Only diagonal / ragged tiles are masked: a wave-uniform branch keeps the v_cmp + v_cndmask
+      // pair per score (a third of this VALU block) off every other tile.
+      if (need_mask) {
+        // tile-relative last visible key of this lane's query
+        const int kmax = (causal ? min(q, S - 1) : S - 1) - kbase - 32 * kb - 4 * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = fast_exp2(sacc[r] * scale_log2 - lse2);
-        p = ((r & 3) + 8 * (r >> 2) <= kmax) ? p : 0.f;
-        sacc[r] = p * (pacc[r] - dlt);  // dS^T
+        for (int r = 0; r < 16; ++r) {
+          float p = fast_exp2(sacc[r] * scale_log2 - lse2);
+          p = ((r & 3) + 8 * (r >> 2) <= kmax) ? p : 0.f;
+          sacc[r] = p * (pacc[r] - dlt);  // dS^T
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[r] = fast_exp2(sacc[r] * scale_log2 - lse2) * (pacc[r] - dlt);
       }
       const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
 #if TH_DQ_AHEAD
@@ -904,19 +911,33 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
       if (!DK) {
         // element r of the lane is query row q0 + 4h + ro (ro = (r&3) + 8(r>>2)), key column
         // `key`: masked iff key > query, i.e. mthr > ro
-        const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform
-        const int mthr = tile_mask ? key - q0 - 4 * h : -0x7fffffff;
+        const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform: only diagonal tiles pay the mask
+        if (tile_mask) {
+          const int mthr = key - q0 - 4 * h;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
-          float4v pv;
+          for (int g = 0; g < 4; ++g) {
+            const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
+            float4v pv;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float p = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
-            pv[e] = mthr > e + 8 * g ? 0.f : p;
-            c[kb][4 * g + e] = pv[e];
+            for (int e = 0; e < 4; ++e) {
+              const float p = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
+              pv[e] = mthr > e + 8 * g ? 0.f : p;
+              c[kb][4 * g + e] = pv[e];
+            }
+            pbuf[(kb * 4 + g) * 64 + lane] = pv;
           }
-          pbuf[(kb * 4 + g) * 64 + lane] = pv;
+        } else {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
+            float4v pv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              pv[e] = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
+              c[kb][4 * g + e] = pv[e];
+            }
+            pbuf[(kb * 4 + g) * 64 + lane] = pv;
+          }
         }
       }
     }
