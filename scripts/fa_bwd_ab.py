@@ -1,5 +1,5 @@
 """Interleaved A/B of flash-backward launch flags at B4 S4096 32/8 heads d128 (causal):
-median ms of the whole backward (delta + dQ + dK/dV) per flag set over 9 rounds."""
+median ms of the whole backward (delta + dQ + dK/dV) per flag set over 9 rounds, then the forward's median."""
 import json
 import os
 import statistics
@@ -29,6 +29,17 @@ for _ in range(9):
         e1.record()
         torch.cuda.synchronize()
         times[f].append(e0.elapsed_time(e1) / 3)
+fwd_t = []
+for _ in range(9):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        flash_fwd(qkv, B, S, Hq, Hkv, D)
+    e1.record()
+    torch.cuda.synchronize()
+    fwd_t.append(e0.elapsed_time(e1) / 3)
+print(json.dumps({"fwd_ms_median": round(statistics.median(fwd_t), 4),
+                  "fwd_tflops": round(4 * B * Hq * S * S * D / 2 / statistics.median(fwd_t) / 1e9, 1)}), flush=True)
 flops = 2.5 * 4 * B * Hq * S * S * D / 2
 for f in flag_sets:
     med = statistics.median(times[f])

@@ -49,9 +49,18 @@ def is_up_to_date() -> bool:
     return LIB.exists() and _stamp_path().exists() and _stamp_path().read_text().strip() == _digest()
 
 
+def source_flags(src: Path) -> list[str]:
+    """Per-source extra flags from a ``// th-build-flags: ...`` line in the file's first 40 lines
+    (e.g. ``-fno-slp-vectorize`` for kernels whose f32 math runs beside MFMAs)."""
+    for line in src.read_text().splitlines()[:40]:
+        if line.startswith("// th-build-flags:"):
+            return line.split(":", 1)[1].split()
+    return []
+
+
 def _compile(src: Path) -> Path:
     obj = BUILD_DIR / (src.stem + ".o")
-    cmd = [HIPCC, *CFLAGS, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *source_flags(src), "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-4000:]}")
