@@ -434,14 +434,26 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   const ushort* dOb = dO + b * bso + (long)hq * HD;
 
   bf16x8 qf[8], gf[8];
+  ushort8 qraw[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    qf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h) : ushort8(0));
+    qraw[s] = q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h) : ushort8(0);
     gf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(dOb + (long)q * ldo + 16 * s + 8 * h) : ushort8(0));
   }
   const long st = ((long)b * Hq + hq) * S;
   const float lse2 = q < S ? LSE[st + q] * LOG2E : INFINITY;
   const float dlt = q < S ? Dl[st + q] : 0.f;
+  // Row constants as the initial accumulators (the query is this lane's for the whole kernel): Q is
+  // prescaled by softmax_scale * log2(e) once (as the forward's PRESCALE variant does), the S chain
+  // starts from -lse2 and the dP chain from -delta, so p = exp2(acc) and dS = p * acc' -- two VALU
+  // per score instead of four (fma, exp, sub, mul).
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qraw[s][e] = f2bf(bf2f(qraw[s][e]) * scale_log2);
+    qf[s] = as_bf(qraw[s]);
+  }
+  const f32x16 s_init = f32x16(-lse2), p_init = f32x16(-dlt);
 
   const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
   const int ntiles = (kv_end + F_BN - 1) / F_BN;
@@ -487,7 +499,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {  // 32-key halves: keeps only one S^T / dP^T pair live
-      f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+      f32x16 sacc = s_init, pacc = p_init;
 #if TH_DQ_AHEAD
       {  // K/V row operands read two k-steps ahead of the MFMAs that use them (2 gaps of latency cover)
         bf16x8 ka[2], va[2];
@@ -525,13 +537,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         const int kmax = (causal ? min(q, S - 1) : S - 1) - kbase - 32 * kb - 4 * h;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = fast_exp2(sacc[r] * scale_log2 - lse2);
+          float p = fast_exp2(sacc[r]);
           p = ((r & 3) + 8 * (r >> 2) <= kmax) ? p : 0.f;
-          sacc[r] = p * (pacc[r] - dlt);  // dS^T
+          sacc[r] = p * pacc[r];  // dS^T = P (dP - delta)
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[r] = fast_exp2(sacc[r] * scale_log2 - lse2) * (pacc[r] - dlt);
+        for (int r = 0; r < 16; ++r) sacc[r] = fast_exp2(sacc[r]) * pacc[r];
       }
       const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
 #if TH_DQ_AHEAD
@@ -773,10 +785,19 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
   const int key = k0 + c32;
   // dK role: V fragments (dP = dO V^T); dV role: K fragments (S = Q K^T)
   const ushort* fb = DK ? Vb : Kb;
+  // Row constants as the initial accumulators: the tile buffer holds -lse2 and -delta per query,
+  // the S chain (dV role) starts from -lse2 with K prescaled by softmax_scale * log2(e) and the dP
+  // chain (dK role) from -delta, so p = exp2(S') and dS = p * dP' (no fma / sub per score).
   bf16x8 kf[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-    kf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
+  for (int s = 0; s < 8; ++s) {
+    ushort8 u = key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0);
+    if (!DK) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
+    }
+    kf[s] = as_bf(u);
+  }
   f32x16 acc[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
@@ -839,8 +860,9 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
   auto write_ld = [&](int buf) {
     if (DK && tid < C_BQ) {
       float* l = reinterpret_cast<float*>(smem + buf * KC_TILE + 2 * C_BQ * 256);
-      l[tid] = DMA ? (lq < S ? lr * LOG2E : INFINITY) : lr * LOG2E;  // rows past S: P = 0 exactly
-      l[C_BQ + tid] = DMA ? (lq < S ? dr : 0.f) : dr;
+      // negated (initial accumulators); rows past S: -inf -> P = 0 exactly
+      l[tid] = DMA ? (lq < S ? -lr * LOG2E : -INFINITY) : -lr * LOG2E;
+      l[C_BQ + tid] = DMA ? (lq < S ? -dr : 0.f) : -dr;
     }
   };
   int lh = 0, lt = 0;  // tile of the lse / delta registers (DMA mode)
@@ -898,6 +920,15 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
       const int q0 = qbase + 32 * kb;
       c[kb] = f32x16(0.f);
       if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
+      {  // -delta (dK role) / -lse2 (dV role) of the half's 32 query rows, in accumulator order
+        const float* rowc = (DK ? ds : ls) + 32 * kb + 4 * h;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4v v4 = *reinterpret_cast<const float4v*>(rowc + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = v4[e];
+        }
+      }
       const char* img = DK ? gs : qs;
       bf16x8 xa[2];
 #pragma unroll
@@ -916,14 +947,14 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
         // `key`: masked iff key > query, i.e. mthr > ro
         const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform: only diagonal tiles pay the mask
         if (tile_mask) {
+          asm volatile("" ::: "memory");  // keeps this a branch: merged, every tile paid the select
           const int mthr = key - q0 - 4 * h;
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
             float4v pv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float p = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
+              const float p = fast_exp2(c[kb][4 * g + e]);
               pv[e] = mthr > e + 8 * g ? 0.f : p;
               c[kb][4 * g + e] = pv[e];
             }
@@ -932,11 +963,10 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
         } else {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
             float4v pv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              pv[e] = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
+              pv[e] = fast_exp2(c[kb][4 * g + e]);
               c[kb][4 * g + e] = pv[e];
             }
             pbuf[(kb * 4 + g) * 64 + lane] = pv;
@@ -957,9 +987,8 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4v pv = pbuf[(kb * 4 + g) * 64 + lane];
-          const float4v dv4 = *reinterpret_cast<const float4v*>(ds + 32 * kb + 4 * h + 8 * g);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = pv[e] * (c[kb][4 * g + e] - dv4[e]);
+          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = pv[e] * c[kb][4 * g + e];  // dS = P (dP - delta)
         }
       }
       const bf16x8 s0 = pack8(c[kb], 0), s1 = pack8(c[kb], 8);
