@@ -252,6 +252,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 #pragma unroll
   for (int d = 0; d < 4; ++d) o[d] = f32x16(0.f);
   float m_i = -INFINITY, l_i = 0.f;
+  // DEFER + PRESCALE: the S chain starts from -m_base (the max the exponentials are taken against,
+  // 0 before the first tile), so a tile that keeps the deferred max needs p = exp2(acc) only --
+  // no subtraction per score; a rescale (rare) shifts the tile's scores once and moves m_base.
+  constexpr bool SHIFT = DEFER && PRESCALE;
+  float m_base = 0.f;
+  f32x16 s_init = f32x16(0.f);
 
   for (int j = 0; j < ntiles; ++j) {
     char* ks = smem + (DBUF ? (j & 1) : 0) * (2 * F_BN * 256);
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     }
     const int kbase = j * F_BN;
     if (!(causal && kbase > q0 + 31)) {  // wave-uniform: tile entirely above the diagonal is skipped
-      f32x16 sacc[2] = {f32x16(0.f), f32x16(0.f)};
+      f32x16 sacc[2] = {s_init, s_init};
       {  // K-row operands are read one k-step ahead of the MFMAs that use them
         FA_PRIO(1);
         bf16x8 a0 = lds_row(ks, c32, h), a1 = lds_row(ks, 32 + c32, h);
@@ -311,7 +317,24 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[kb][r]);
       mt = half_swap_max(mt);
       float m_use;
-      if (DEFER) {
+      if (SHIFT) {
+        // scores are relative to m_base here: mt + m_base is the tile's true max
+        if (!__all(mt + m_base - m_i <= F_DEFER_THR)) {
+          const float m_new = fmaxf(m_i, mt + m_base);
+          const float mu = m_new == -INFINITY ? 0.f : m_new;
+          const float alpha = fast_exp2(m_i - mu);
+          l_i *= alpha;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) o[d] *= alpha;
+          m_i = m_new;
+          const float shift = mu - m_base;  // rebase this tile's scores and the next tiles' chains
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) sacc[kb] -= shift;
+          m_base = mu;
+          s_init = f32x16(-mu);
+        }
+        m_use = 0.f;  // sacc already holds s - m_base
+      } else if (DEFER) {
         if (!__all(mt - m_i <= F_DEFER_THR)) {  // some query's max moved too far: rescale now
           const float m_new = fmaxf(m_i, mt);
           const float mu = m_new == -INFINITY ? 0.f : m_new;
@@ -331,15 +354,16 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         for (int d = 0; d < 4; ++d) o[d] *= alpha;
         m_i = m_new;
       }
-      float rs = 0.f;
+      float rs4[4] = {0.f, 0.f, 0.f, 0.f};  // 4 partial row sums: no 32-deep dependent add chain
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(sacc[kb][r] - m_use);
+          const float p = fast_exp2(SHIFT ? sacc[kb][r] : sacc[kb][r] - m_use);
           sacc[kb][r] = p;
-          rs += p;
+          rs4[r & 3] += p;
         }
+      const float rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
       l_i += half_swap_sum(rs);
       bf16x8 pf[4];
 #pragma unroll
