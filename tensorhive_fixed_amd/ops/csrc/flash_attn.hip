@@ -942,16 +942,15 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int q0 = qbase + 32 * kb;
-      c[kb] = f32x16(0.f);
+      // (no zero fill: a skipped half is skipped again in phase 2, and a dead value costs no copies)
       if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
       {  // -delta (dK role) / -lse2 (dV role) of the half's 32 query rows, in accumulator order
         const float* rowc = (DK ? ds : ls) + 32 * kb + 4 * h;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4v v4 = *reinterpret_cast<const float4v*>(rowc + 8 * g);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = v4[e];
-        }
+        const float4v r0 = *reinterpret_cast<const float4v*>(rowc), r1 = *reinterpret_cast<const float4v*>(rowc + 8),
+                      r2 = *reinterpret_cast<const float4v*>(rowc + 16), r3 = *reinterpret_cast<const float4v*>(rowc + 24);
+        c[kb] = __builtin_shufflevector(__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                        __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4, 5, 6,
+                                        7, 8, 9, 10, 11, 12, 13, 14, 15);
       }
       const char* img = DK ? gs : qs;
       bf16x8 xa[2];
