@@ -35,16 +35,22 @@ def main():
         o1 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         o2 = torch.empty_like(o1)
         variants = {"hipblaslt": lambda: torch.mm(a.t(), b, out=o1)}
-        for sk in sorted({1, 2, default_splitk(M, N, T)}):
-            for pp in (1, 2, 4):
+        pps = [int(x) for x in os.environ.get("TN_PP", "1,2,4").split(",")]
+        sks = sorted({1, 2, default_splitk(M, N, T)}) if os.environ.get("TN_ALL_SPLITK", "1") == "1" \
+            else [default_splitk(M, N, T)]
+        for sk in sks:
+            for pp in pps:
                 variants[f"tn_s{pp}_sk{sk}"] = (lambda sk=sk, pp=pp: gemm_tn_(a, b, o2, splitk=sk, pingpong=pp))
         res = {k: [] for k in variants}
         for _ in range(3):
             for k, fn in variants.items():
                 res[k].append(timed(fn))
-        gemm_tn_(a, b, o2, splitk=1)
         torch.mm(a.t(), b, out=o1)
-        err = ((o1.float() - o2.float()).abs().max() / o1.float().abs().max()).item()
+        errs = {}
+        for pp in pps:
+            gemm_tn_(a, b, o2, splitk=1, pingpong=pp)
+            errs[pp] = round(((o1.float() - o2.float()).abs().max() / o1.float().abs().max()).item(), 5)
+        err = max(errs.values())
         fl = 2.0 * M * N * T
         print(json.dumps({"gemm": name, "M": M, "N": N, "K": T, "rel_err_vs_hipblaslt": round(err, 5),
                           "default_splitk": default_splitk(M, N, T),

@@ -66,6 +66,11 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // Stage k-rows [k0, k0+64) of a [K][ld] operand, columns [c0, c0+256), into a lane-linear LDS
 // image whose (row, 64-B chunk c) holds global chunk c ^ (row & 3).  Wave-instruction u writes LDS
 // bytes [u*1KB, +1KB) = rows 2u, 2u+1; a lane's byte offset from the wave-uniform row base depends
@@ -365,7 +370,10 @@ __device__ __forceinline__ void wait_dma_barrier(int n) {
 // AHEAD = how many k-tiles ahead each group's DMA runs (2: two slots of lead time per tile, 3: four;
 // with 3 the stage a DMA overwrites was gathered one slot earlier, so G1 retires its reads
 // (lgkmcnt(0)) before its gather slot ends)
-template <bool SPLIT, int AHEAD>
+// MI16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (one k-step per 32-deep k-tile, 8 x 4 blocks of
+// 16 x 16 per wave).  Operand of lane l: column (l & 15) of a 16-column block, k rows 8 (l >> 4) .. +7,
+// one tr_pair (rows 8g + q and 8g + 4 + q of the 16-lane group g, columns 4p .. 4p + 3 of the block).
+template <bool SPLIT, int AHEAD, bool MI16 = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
     ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
@@ -400,12 +408,33 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
   for (int mb = 0; mb < 4; ++mb) a_off[mb] = lane_base + ((((wm * 128 + 32 * mb) >> 5) ^ q) << 6);
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) b_off[nb] = lane_base + ((((wn * 64 + 32 * nb) >> 5) ^ q) << 6);
+  // MI16 offsets: row 8g + q, 64-B chunk (col >> 5) ^ q, byte (col & 31) * 2 + 8p inside it
+  const int lane_base16 = (8 * g + q) * ROWB + 8 * p;
+  int a_off16[8], b_off16[4];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+    const int col = wm * 128 + 16 * mb;
+    a_off16[mb] = lane_base16 + (((col >> 5) ^ q) << 6) + (col & 31) * 2;
+  }
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int col = wn * 64 + 16 * nb;
+    b_off16[nb] = lane_base16 + (((col >> 5) ^ q) << 6) + (col & 31) * 2;
+  }
 
-  f32x16 acc[4][2];
+  f32x16 acc[MI16 ? 1 : 4][MI16 ? 1 : 2];
+  f32x4 acc16[MI16 ? 8 : 1][MI16 ? 4 : 1];
+  if constexpr (MI16) {
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+    for (int mb = 0; mb < 8; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
+      for (int nb = 0; nb < 4; ++nb) acc16[mb][nb] = f32x4(0.f);
+  } else {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
+  }
 
   const unsigned lds0 = (unsigned)(uintptr_t)smem;
   const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
@@ -421,6 +450,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
   if (g1) asm volatile("s_barrier" ::: "memory");  // G1 enters one slot late
 
   bf16x8 af[4][2], bf[2][2];
+  bf16x8 af16[MI16 ? 8 : 1], bf16[MI16 ? 4 : 1];
   for (int t = 0; t < nt; ++t) {
     // DMAs younger than k-tile t+1's that are in flight at the end of this iteration
     const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
@@ -432,13 +462,20 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     }
     const char LDS_AS* sa = smem + (t & (NSTAGE2 - 1)) * STAGEB2;
     const char LDS_AS* sb = sa + OPB2;
+    if constexpr (MI16) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int ko = ks * 16 * ROWB;
+      for (int mb = 0; mb < 8; ++mb) af16[mb] = tr_pair(sa + a_off16[mb], sa + a_off16[mb] + 4 * ROWB);
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) af[mb][ks] = tr_pair(sa + a_off[mb] + ko, sa + a_off[mb] + ko + 4 * ROWB);
+      for (int nb = 0; nb < 4; ++nb) bf16[nb] = tr_pair(sb + b_off16[nb], sb + b_off16[nb] + 4 * ROWB);
+    } else {
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ko = ks * 16 * ROWB;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) af[mb][ks] = tr_pair(sa + a_off[mb] + ko, sa + a_off[mb] + ko + 4 * ROWB);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
+      }
     }
     if (g1) {  // G1's B image of k-tile t+1 must land before G0 gathers it (next slot)
       if (AHEAD >= 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -447,12 +484,19 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
       asm volatile("s_barrier" ::: "memory");
     }
     // ---- compute slot
+    if constexpr (MI16) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int mb = 0; mb < 8; ++mb)
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
+        for (int nb = 0; nb < 4; ++nb) acc16[mb][nb] = mfma16(af16[mb], bf16[nb], acc16[mb][nb]);
+    } else {
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
+    }
     __builtin_amdgcn_sched_barrier(0);
     if (!g1) {  // G0's A image of k-tile t+1 landed before the barrier that opens its gather
       wait_dma_barrier(younger);
@@ -462,6 +506,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
   }
   if (!g1) asm volatile("s_barrier" ::: "memory");
 
+  if constexpr (MI16) {  // 16x16 result: lane l holds column (l & 15), rows 4 (l >> 4) + r
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const long n = n0 + wn * 64 + 16 * nb + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long m = m0 + wm * 128 + 16 * mb + 4 * (lane >> 4) + r;
+          if (SPLIT) {
+            slab[((long)split * M + m) * N + n] = acc16[mb][nb][r];
+          } else {
+            float v = acc16[mb][nb][r];
+            if (beta) v += bf2f(C[m * ldc + n]);
+            C[m * ldc + n] = f2bf(v);
+          }
+        }
+      }
+    return;
+  }
   const int c32 = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
@@ -665,7 +729,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop;
 //        bit1 = ping-pong v2 (k-tiles of 32, 4-stage ring, per-group DMA two k-tiles ahead);
 //        bit2 (with bit1) = DMA three k-tiles ahead;
-//        bit3 = one wave per SIMD, 128 x 128 per wave (gemm_tn_w4_kernel, 256 threads)
+//        bit3 = one wave per SIMD, 128 x 128 per wave (gemm_tn_w4_kernel, 256 threads);
+//        bit4 (with bit1) = v_mfma_f32_16x16x32_bf16 fragments in the ping-pong v2 kernel
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -686,7 +751,10 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
   } while (0)
 #define TH_TN_LAUNCH2(KERNEL, AH)                                                                \
   do {                                                                                          \
-    if (splitk > 1) KERNEL<true, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
+    if (flags & 16) {                                                                           \
+      if (splitk > 1) KERNEL<true, AH, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
+      else KERNEL<false, AH, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
+    } else if (splitk > 1) KERNEL<true, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
     else KERNEL<false, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
   } while (0)
   if (flags & 8) {
