@@ -360,6 +360,25 @@ __device__ __forceinline__ void stage_op2(const ushort* __restrict__ g, const La
   }
 }
 
+// SW images: 64-B chunk c of k-row r holds global chunk c ^ S(r), S(r) = (r + (r >> 3)) & 3, so rows 8
+// apart (the two 16-lane groups of a half in the 16x16x32 operand read) land on different banks.
+// Wave-instruction u = 4i + w4 writes rows 2u, 2u+1: S depends on the lane half, u & 1 (= w4 & 1)
+// and i, so a wave needs one offset per i.
+__device__ __forceinline__ unsigned lane_off_sw(long ld, long c0, int lane, int w4, int i) {
+  const int hi = lane >> 5, slot = lane & 31;
+  const int u = 4 * i + w4, row = 2 * u + hi;
+  const int chunk = (slot >> 2) ^ ((row + (row >> 3)) & 3);
+  return (unsigned)(2 * ((long)hi * ld + c0 + chunk * 32 + (slot & 3) * 8));
+}
+__device__ __forceinline__ void stage_op2_sw(const ushort* __restrict__ g, const unsigned (&lo)[4], long ld,
+                                             long k0, unsigned img, int w4) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = i * 4 + w4;
+    glds16(g + (k0 + 2 * u) * ld, lo[i], img + u * 1024);
+  }
+}
+
 // vmcnt(4 * n) with n in 0..2 (immediate operand)
 __device__ __forceinline__ void wait_dma_barrier(int n) {
   if (n >= 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
@@ -373,7 +392,7 @@ __device__ __forceinline__ void wait_dma_barrier(int n) {
 // MI16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (one k-step per 32-deep k-tile, 8 x 4 blocks of
 // 16 x 16 per wave).  Operand of lane l: column (l & 15) of a 16-column block, k rows 8 (l >> 4) .. +7,
 // one tr_pair (rows 8g + q and 8g + 4 + q of the 16-lane group g, columns 4p .. 4p + 3 of the block).
-template <bool SPLIT, int AHEAD, bool MI16 = false>
+template <bool SPLIT, int AHEAD, bool MI16 = false, bool SW = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
     ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk,
@@ -403,23 +422,29 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
 
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int lane_base = (8 * (g >> 1) + q) * ROWB + 32 * (g & 1) + 8 * p;
-  int a_off[4], b_off[2];
+  // 32x32 operand rows 16 ks + 8h + q (+4): XOR q, or S = (q + 2 ks + h) & 3 with SW
+  int a_off[4][2], b_off[2][2];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) a_off[mb] = lane_base + ((((wm * 128 + 32 * mb) >> 5) ^ q) << 6);
+  for (int ks = 0; ks < 2; ++ks) {
+    const int x = SW ? (q + 2 * ks + (g >> 1)) & 3 : q;
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) b_off[nb] = lane_base + ((((wn * 64 + 32 * nb) >> 5) ^ q) << 6);
+    for (int mb = 0; mb < 4; ++mb) a_off[mb][ks] = lane_base + ((((wm * 128 + 32 * mb) >> 5) ^ x) << 6) + ks * 16 * ROWB;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) b_off[nb][ks] = lane_base + ((((wn * 64 + 32 * nb) >> 5) ^ x) << 6) + ks * 16 * ROWB;
+  }
   // MI16 offsets: row 8g + q, 64-B chunk (col >> 5) ^ q, byte (col & 31) * 2 + 8p inside it
   const int lane_base16 = (8 * g + q) * ROWB + 8 * p;
+  const int x16 = SW ? (q + g) & 3 : q;  // rows 8g + q (+4)
   int a_off16[8], b_off16[4];
 #pragma unroll
   for (int mb = 0; mb < 8; ++mb) {
     const int col = wm * 128 + 16 * mb;
-    a_off16[mb] = lane_base16 + (((col >> 5) ^ q) << 6) + (col & 31) * 2;
+    a_off16[mb] = lane_base16 + (((col >> 5) ^ x16) << 6) + (col & 31) * 2;
   }
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb) {
     const int col = wn * 64 + 16 * nb;
-    b_off16[nb] = lane_base16 + (((col >> 5) ^ q) << 6) + (col & 31) * 2;
+    b_off16[nb] = lane_base16 + (((col >> 5) ^ x16) << 6) + (col & 31) * 2;
   }
 
   f32x16 acc[MI16 ? 1 : 4][MI16 ? 1 : 2];
@@ -438,12 +463,26 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
 
   const unsigned lds0 = (unsigned)(uintptr_t)smem;
   const LaneOffs pa = lane_offs(lda, m0, lane), pb = lane_offs(ldb, n0, lane);
+  unsigned pa_sw[4], pb_sw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pa_sw[i] = SW ? lane_off_sw(lda, m0, lane, w4, i) : 0u;
+    pb_sw[i] = SW ? lane_off_sw(ldb, n0, lane, w4, i) : 0u;
+  }
+  auto stage_a = [&](long k0, unsigned img) {
+    if (SW) stage_op2_sw(A, pa_sw, lda, k0, img, w4);
+    else stage_op2(A, pa, lda, k0, img, w4);
+  };
+  auto stage_b = [&](long k0, unsigned img) {
+    if (SW) stage_op2_sw(B, pb_sw, ldb, k0, img, w4);
+    else stage_op2(B, pb, ldb, k0, img, w4);
+  };
   // prologue: k-tiles 0 .. AHEAD-1 (A by G0, B by G1), all landed before the first slot
 #pragma unroll
   for (int j = 0; j < AHEAD; ++j) {
     if (j < nt) {
-      if (!g1) stage_op2(A, pa, lda, kbeg + j * TK2, lds0 + j * STAGEB2, w4);
-      else stage_op2(B, pb, ldb, kbeg + j * TK2, lds0 + j * STAGEB2 + OPB2, w4);
+      if (!g1) stage_a(kbeg + j * TK2, lds0 + j * STAGEB2);
+      else stage_b(kbeg + j * TK2, lds0 + j * STAGEB2 + OPB2);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -457,8 +496,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     // ---- gather slot (+ this group's DMA AHEAD k-tiles ahead)
     if (t + AHEAD < nt) {
       const unsigned st = lds0 + ((t + AHEAD) & (NSTAGE2 - 1)) * STAGEB2;
-      if (!g1) stage_op2(A, pa, lda, kbeg + (long)(t + AHEAD) * TK2, st, w4);
-      else stage_op2(B, pb, ldb, kbeg + (long)(t + AHEAD) * TK2, st + OPB2, w4);
+      if (!g1) stage_a(kbeg + (long)(t + AHEAD) * TK2, st);
+      else stage_b(kbeg + (long)(t + AHEAD) * TK2, st + OPB2);
     }
     const char LDS_AS* sa = smem + (t & (NSTAGE2 - 1)) * STAGEB2;
     const char LDS_AS* sb = sa + OPB2;
@@ -470,11 +509,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
     } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int ko = ks * 16 * ROWB;
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb) af[mb][ks] = tr_pair(sa + a_off[mb] + ko, sa + a_off[mb] + ko + 4 * ROWB);
+        for (int mb = 0; mb < 4; ++mb) af[mb][ks] = tr_pair(sa + a_off[mb][ks], sa + a_off[mb][ks] + 4 * ROWB);
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb] + ko, sb + b_off[nb] + ko + 4 * ROWB);
+        for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = tr_pair(sb + b_off[nb][ks], sb + b_off[nb][ks] + 4 * ROWB);
       }
     }
     if (g1) {  // G1's B image of k-tile t+1 must land before G0 gathers it (next slot)
@@ -730,7 +768,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 //        bit1 = ping-pong v2 (k-tiles of 32, 4-stage ring, per-group DMA two k-tiles ahead);
 //        bit2 (with bit1) = DMA three k-tiles ahead;
 //        bit3 = one wave per SIMD, 128 x 128 per wave (gemm_tn_w4_kernel, 256 threads);
-//        bit4 (with bit1) = v_mfma_f32_16x16x32_bf16 fragments in the ping-pong v2 kernel
+//        bit4 (with bit1) = v_mfma_f32_16x16x32_bf16 fragments in the ping-pong v2 kernel;
+//        bit5 (with bit1) = row swizzle S(r) = (r + (r >> 3)) & 3 of the v2 images
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -751,7 +790,13 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
   } while (0)
 #define TH_TN_LAUNCH2(KERNEL, AH)                                                                \
   do {                                                                                          \
-    if (flags & 16) {                                                                           \
+    if ((flags & 48) == 48) {                                                                   \
+      if (splitk > 1) KERNEL<true, AH, true, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
+      else KERNEL<false, AH, true, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
+    } else if (flags & 32) {                                                                    \
+      if (splitk > 1) KERNEL<true, AH, false, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
+      else KERNEL<false, AH, false, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
+    } else if (flags & 16) {                                                                    \
       if (splitk > 1) KERNEL<true, AH, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
       else KERNEL<false, AH, true><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
     } else if (splitk > 1) KERNEL<true, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
