@@ -30,6 +30,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
+#ifndef TH_TN_GM
+#define TH_TN_GM 8  // output-tile rows per XCD band in the ping-pong v2 order
+#endif
 namespace {
 constexpr int TM = 256, TN = 256, TK = 64;
 constexpr int NTHR = 512;
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_tn_pp2_kernel(
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = SPLIT ? L / splitk : L;
   const int split = SPLIT ? L % splitk : 0;
-  constexpr int GM = 8;
+  constexpr int GM = TH_TN_GM;
   const int per_band = GM * nN;
   const int band = tile / per_band;
   const int first_m = band * GM;
