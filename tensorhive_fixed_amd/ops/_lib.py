@@ -45,7 +45,6 @@ _SIGS: dict[str, list] = {
     "th_flash_attn_fwd": [P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, I, P],
     "th_flash_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, I, P],
     "th_embedding_bwd": [P, P, P, P, L, I, I, P],
-    "th_probe_run": [P, I, I, I, P],
     "th_transpose_bf16": [P, P, L, L, L, I, P],
     "th_gemm_tn": [P, L, P, L, P, L, I, I, I, I, I, P, I, P],
     "th_gemm_nt": [P, L, P, L, P, L, I, I, I, I, I, P],
