@@ -34,3 +34,18 @@ def test_library_exports_every_bound_entry_point():
     exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
     missing = sorted(name for name in _lib._SIGS if name not in exported)
     assert not missing, f"bound in ops/_lib.py but not exported by libthk.so: {missing}"
+
+
+def test_bindings_match_the_c_declarations():
+    """Argument counts of every ops/_lib.py binding equal those of its `extern "C"` definition."""
+    import re
+
+    decls = {}
+    for src in build._sources():
+        text = src.read_text()
+        for m in re.finditer(r'extern "C" \w+\s+(th_\w+)\(([^)]*)\)', text):
+            args = [a for a in m.group(2).replace("\n", " ").split(",") if a.strip() and a.strip() != "void"]
+            decls[m.group(1)] = len(args)
+    for name, argtypes in _lib._SIGS.items():
+        assert name in decls, f"{name}: no extern \"C\" definition in ops/csrc"
+        assert decls[name] == len(argtypes), f"{name}: C takes {decls[name]} args, binding has {len(argtypes)}"
