@@ -4,12 +4,43 @@
 // tests/test_webapp_cli.py runs them under node against the Python implementations.
 "use strict";
 
-// One shell word per value, as the server renders it (models/orm.py _shell_value): values the
-// shell would split or strip (TF_CONFIG JSON, spaces, quotes, operators) are single-quoted.
-const SHELL_SPECIAL = /[\s"'{}\[\];&|<>()\\*?!#`]/;
+// One shell word per value, as the server renders it (models/orm.py _shell_value): a value the
+// shell already reads as one word stays as typed (the user's own quoting, globs, $VARS); values
+// that would split, have an unbalanced quote or an unquoted operator, and JSON documents
+// (TF_CONFIG), are single-quoted.  isOneShellWord mirrors _is_one_shell_word line for line.
+export function isOneShellWord(v) {
+  let words = 0, inWord = false, quote = "", i = 0;
+  while (i < v.length) {
+    const c = v[i];
+    if (quote === "'") {
+      if (c === "'") quote = "";
+    } else if (quote === '"') {
+      if (c === "\\") i += 1;
+      else if (c === '"') quote = "";
+    } else if (" \t\n".includes(c)) {
+      inWord = false;
+    } else if (";&|<>()".includes(c)) {
+      return false;
+    } else {
+      if (!inWord) { words += 1; inWord = true; }
+      if (c === "\\") i += 1;
+      else if (c === "'" || c === '"') quote = c;
+    }
+    i += 1;
+  }
+  return words === 1 && quote === "" && i === v.length;
+}
+
+function isJsonDocument(v) {
+  const t = v.trimStart();
+  if (!(t.startsWith("{") || t.startsWith("["))) return false;
+  try { JSON.parse(v); return true; } catch (e) { return false; }
+}
+
 export function shellValue(v) {
   v = v === undefined || v === null ? "" : String(v);
-  return SHELL_SPECIAL.test(v) ? "'" + v.replace(/'/g, "'\\''") + "'" : v;
+  if (v === "" || (isOneShellWord(v) && !isJsonDocument(v))) return v;
+  return "'" + v.replace(/'/g, "'\\''") + "'";
 }
 
 // ENV=v ... command param value ...; a parameter whose name ends with "=" (or " ") is joined

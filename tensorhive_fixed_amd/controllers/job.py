@@ -339,7 +339,11 @@ def _placements(form: dict) -> list[dict]:
         gpus = p.get("gpus", [p["gpu"]] if "gpu" in p else [])
         count = p.get("gpuCount")
         if isinstance(gpus, str) and gpus.startswith("auto"):  # "auto:4": the scheduler picks
-            count = int(gpus.split(":", 1)[1]) if ":" in gpus else count
+            if ":" in gpus:
+                n = gpus.split(":", 1)[1]
+                assert n.isdigit(), "auto placement needs a count: auto:N"
+                count = int(n)
+            assert count is not None, "auto placement needs a count: auto:N or gpuCount"
             gpus = []
         if count is not None:
             assert isinstance(count, int) and count >= 1, "gpuCount must be a positive integer"
@@ -372,6 +376,11 @@ def generate_tasks(id: int, form: dict):
     assert job.status is not JobStatus.running, "must be stopped first"
     pl = _placements(form)
     kind = form["template"]
+    # Only torchrun defers device choice to the allocator (one task owns all its devices); the
+    # per-GPU templates need concrete indices -- a count there would pin every task to GPU 0 or
+    # create no task at all.
+    assert kind == "torchrun" or all(p["count"] is None for p in pl), \
+        "gpuCount / auto:N placements are supported by the torchrun template only"
     command = form.get("command") or "python train.py"
     master = pl[0]["hostname"]
     if kind == "torchrun":

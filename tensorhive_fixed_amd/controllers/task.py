@@ -81,7 +81,11 @@ def synchronize(task_id: int, cache: SessionCache | None = None) -> None:
             return
         if task.job_id in allocation.launching or allocation.launched_at.get(task.job_id, -1.0) >= fetched:
             return
-        if task.pid is None or task.pid not in live:
+        # By session name first: it survives any number of restarts, whatever pid was stored.
+        sess = live.get(task_nursery.session_name(task.id)) if task.pid is not None else None
+        if sess is None and task.pid is not None:
+            sess = live.get(task.pid)
+        if sess is None:
             if task.status is TaskStatus.running:
                 task.status = TaskStatus.terminated
             elif task.status is TaskStatus.unsynchronized:
@@ -90,7 +94,6 @@ def synchronize(task_id: int, cache: SessionCache | None = None) -> None:
             task.save()
             allocation.release_task(task.id)  # the task's devices are free again
         else:
-            sess = live[task.pid]
             if isinstance(sess, dict):  # the restart policy may have replaced the process
                 cur = int(sess.get("pid") or task.pid)
                 if cur != task.pid:

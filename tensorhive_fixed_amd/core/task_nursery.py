@@ -142,14 +142,28 @@ def running_pids(hostname: str, user: str) -> list[int]:
     return [int(d["pid"]) for d in running(hostname, user)]
 
 
-def running_sessions(hostname: str, user: str) -> dict[int, dict]:
-    """Live sessions keyed by every pid a task is known by: its current pid and, for a session
-    the restart policy has restarted, the pid it was spawned with (what the daemon stored)."""
-    out: dict[int, dict] = {}
+def _pid_history(d: dict) -> list[int]:
+    pids = [int(d["pid"])]
+    for k in ("first_pid", "pgid"):
+        if d.get(k) not in (None, ""):
+            pids.append(int(d[k]))
+    for p in str(d.get("pids") or "").split(","):
+        if p.strip().isdigit():
+            pids.append(int(p))
+    return pids
+
+
+def running_sessions(hostname: str, user: str) -> dict:
+    """Live sessions keyed by their session name (``tensorhive_task_<id>``) and by every pid the
+    task has run as: the spawn-time pid, each restart's pid (th-run's ``pids`` history) and the
+    current one.  A daemon that stored any of them -- or none, after a restart -- finds the session."""
+    out: dict = {}
     for d in running(hostname, user):
-        out[int(d["pid"])] = d
-        if d.get("first_pid") not in (None, ""):
-            out.setdefault(int(d["first_pid"]), d)
+        out[str(d.get("name"))] = d
+        cur = int(d["pid"])
+        out[cur] = d
+        for p in _pid_history(d):
+            out.setdefault(p, d)
     return out
 
 

@@ -247,7 +247,7 @@ class SimulatedNode(FakeTransport):
             pid = self._next
             self._next += 1
             self.sessions[pid] = {"name": name, "pid": pid, "pgid": pid, "started": time.time(), "user": user,
-                                  "command": cmd, "log": logf, "gpus": gpus, "first_pid": pid, "restarts": 0,
+                                  "command": cmd, "log": logf, "gpus": gpus, "first_pid": pid, "pids": str(pid), "restarts": 0,
                                   "max_restarts": max_restarts, "env": env}
             self.logs[logf] = [f"[simulated] {cmd}"]
         if self.telemetry is not None:
@@ -270,7 +270,8 @@ class SimulatedNode(FakeTransport):
             self.sessions.pop(pid, None)
             new = self._next
             self._next += 1
-            s = dict(s, pid=new, pgid=new, restarts=s["restarts"] + 1, last_exit_code=code)
+            s = dict(s, pid=new, pgid=new, restarts=s["restarts"] + 1, last_exit_code=code,
+                     pids=f"{s['pids']},{new}")
             self.sessions[new] = s
             self.logs.setdefault(s["log"], []).append(
                 f"[th-run] exit code {code}; restart {s['restarts']}/{s['max_restarts']}")
@@ -290,7 +291,8 @@ class SimulatedNode(FakeTransport):
 
     def _signal(self, pid: int, verb: str, user) -> Result:
         with self._lock:
-            s = self.sessions.get(pid) or next((x for x in self.sessions.values() if x.get("first_pid") == pid), None)
+            s = self.sessions.get(pid) or next(
+                (x for x in self.sessions.values() if str(pid) in str(x.get("pids", "")).split(",")), None)
             pid = s["pid"] if s else pid
         if s is None or (user and s["user"] != user):
             return Result(self.host, "", f"no such session {pid}", 1)

@@ -19,8 +19,10 @@ from __future__ import annotations
 
 import datetime
 import enum
+import json
 import logging
 import re
+import shlex
 import threading
 from datetime import timedelta
 
@@ -50,13 +52,58 @@ def _utcnow():
     return dates.utcnow()
 
 
-_SHELL_SPECIAL = re.compile(r"""[\s"'{}\[\];&|<>()\\*?!#`]""")
+def _is_one_shell_word(v: str) -> bool:
+    """Would ``bash`` read ``v`` as exactly one word with no unquoted control operator?
+    (A small scanner, mirrored line for line by ``app/static/js/launch.js``.)"""
+    words, in_word, quote, i = 0, False, "", 0
+    while i < len(v):
+        c = v[i]
+        if quote == "'":
+            if c == "'":
+                quote = ""
+        elif quote == '"':
+            if c == "\\":
+                i += 1
+            elif c == '"':
+                quote = ""
+        elif c in " \t\n":
+            in_word = False
+        elif c in ";&|<>()":
+            return False
+        else:
+            if not in_word:
+                words, in_word = words + 1, True
+            if c == "\\":
+                i += 1
+            elif c in "'\"":
+                quote = c
+        i += 1
+    return words == 1 and quote == "" and i == len(v)
+
+
+def _is_json_document(v: str) -> bool:
+    if not v.lstrip().startswith(("{", "[")):
+        return False
+    try:
+        json.loads(v)
+        return True
+    except ValueError:
+        return False
 
 
 def _shell_value(v) -> str:
-    """A command-segment value as one shell word (see Task.render)."""
+    """A command-segment value as one shell word (see Task.render).
+
+    A value that the shell already reads as exactly ONE word is left untouched, so values the
+    user quoted themselves (``"a b"``), globs (``/data/*.tfrecord``) and ``$VARS`` keep the
+    reference's semantics (``models/Task.py:77-98`` pasted values verbatim).  Single-quoted are
+    only: a value that would split into several words, has an unbalanced quote or an unquoted
+    control operator (``;`` ``&`` ``|`` ``<`` ``>`` parentheses), and a JSON document (a
+    generated TF_CONFIG), whose quotes are data rather than shell syntax."""
     v = "" if v is None else str(v)
-    return "'" + v.replace("'", "'\\''") + "'" if _SHELL_SPECIAL.search(v) else v
+    if not v or (_is_one_shell_word(v) and not _is_json_document(v)):
+        return v
+    return "'" + v.replace("'", "'\\''") + "'"
 
 
 # ------------------------------------------------------------------------------------ users
@@ -872,9 +919,10 @@ class Task(CRUDModel, Base):
         """``ENV=v ... command param value ...`` from explicit segment lists (the launch path
         substitutes allocated devices before rendering, see ``core/allocation.py``).
 
-        The line runs under ``bash -lc``: a value the shell would split or strip -- a TF_CONFIG
-        JSON document, anything with spaces, quotes, braces or shell operators -- is single-quoted;
-        plain values stay as typed, so ``$HOME`` or ``~`` in them still expand."""
+        The line runs under ``bash -lc``: a value the shell would split -- unquoted spaces or
+        control operators, an unbalanced quote -- and a TF_CONFIG JSON document are
+        single-quoted; every other value stays as typed, so ``$HOME``, globs and the user's own
+        quoting keep their shell meaning (see ``_shell_value``)."""
         parts = [f"{n}={_shell_value(v)}" for n, v in envs]
         parts.append(self.command)
         for n, v in params:

@@ -339,9 +339,14 @@ int do_spawn(Args& a) {
     st["pid"] = std::to_string((long)c);
     st["pgid"] = std::to_string((long)c);
     if (restarts == 0) st["first_pid"] = std::to_string((long)c);
+    // every incarnation's pid, so a caller holding ANY of them still finds the session
+    st["pids"] += (st["pids"].empty() ? "" : ",") + std::to_string((long)c);
     st["restarts"] = std::to_string(restarts);
     st["status"] = "running";
     write_state(a.state_dir, a.name, st);
+    // A stop requested while this run was being started (after the restart loop's last check)
+    // found no live process group; honour it now so a stopped task never runs to completion.
+    if (restarts > 0 && access(stopf.c_str(), F_OK) == 0) kill(-c, SIGTERM);
     if (restarts == 0) {
       long cpid = (long)c;
       write_all(hs[1], (const char*)&cpid, sizeof cpid);
@@ -399,7 +404,20 @@ bool lookup(const Args& a, KV& kv) {
   return read_state(a.state_dir + "/" + a.name + ".state", kv);
 }
 
-// Name of the session whose current or first pid is `pid` ("" if none).
+bool pid_in_history(KV& kv, long pid) {
+  if (atol(kv["pgid"].c_str()) == pid || atol(kv["first_pid"].c_str()) == pid) return true;
+  const std::string& h = kv["pids"];
+  size_t i = 0;
+  while (i < h.size()) {
+    size_t j = h.find(',', i);
+    if (j == std::string::npos) j = h.size();
+    if (atol(h.substr(i, j - i).c_str()) == pid) return true;
+    i = j + 1;
+  }
+  return false;
+}
+
+// Name of the live session that has ever run as `pid` ("" if none).
 std::string session_of_pid(const std::string& dir, long pid) {
   DIR* d = opendir(dir.c_str());
   if (!d) return "";
@@ -409,9 +427,7 @@ std::string session_of_pid(const std::string& dir, long pid) {
     std::string n = e->d_name;
     if (n.size() < 7 || n.substr(n.size() - 6) != ".state") continue;
     KV kv;
-    if (read_state(dir + "/" + n, kv) && kv["status"] != "exited" &&
-        (atol(kv["pgid"].c_str()) == pid || atol(kv["first_pid"].c_str()) == pid))
-      found = kv["name"];
+    if (read_state(dir + "/" + n, kv) && kv["status"] != "exited" && pid_in_history(kv, pid)) found = kv["name"];
   }
   closedir(d);
   return found;
@@ -420,6 +436,7 @@ std::string session_of_pid(const std::string& dir, long pid) {
 int do_signal(const Args& a, int sig) {
   long pg = a.pid;
   std::string name = a.name;
+  bool restarting = false;
   if (pg <= 0) {
     KV kv;
     if (!lookup(a, kv)) {
@@ -428,11 +445,15 @@ int do_signal(const Args& a, int sig) {
     }
     if (kv["status"] == "exited") return 4;
     pg = atol(kv["pgid"].c_str());
+    restarting = kv["status"] == "restarting";
   } else {
     name = session_of_pid(a.state_dir, pg);
     if (!name.empty()) {  // signal the current incarnation of a restarted task
       KV kv;
-      if (read_state(a.state_dir + "/" + name + ".state", kv)) pg = atol(kv["pgid"].c_str());
+      if (read_state(a.state_dir + "/" + name + ".state", kv)) {
+        pg = atol(kv["pgid"].c_str());
+        restarting = kv["status"] == "restarting";
+      }
     }
   }
   if (!name.empty()) {  // a requested stop is never undone by the restart policy
@@ -441,6 +462,9 @@ int do_signal(const Args& a, int sig) {
   }
   if (pg <= 0) return 3;
   if (kill(-(pid_t)pg, sig) != 0 && kill((pid_t)pg, sig) != 0) {
+    // Between a failed run and its restart there is no process to signal: the stop marker
+    // written above already keeps the next run from starting, so the request succeeded.
+    if (errno == ESRCH && restarting) return 0;
     perror("th-run: kill");
     return 1;
   }

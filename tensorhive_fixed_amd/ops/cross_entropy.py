@@ -62,9 +62,12 @@ class _LinearCE(torch.autograd.Function):
         dh = torch.empty_like(h2)
         loss_sum = torch.zeros((), device=h2.device, dtype=torch.float32)
         mg = getattr(w, "main_grad", None)
-        f32_main = mg is not None and mg.dtype != w.dtype  # TH_GRAD_FP32: GEMMs write bf16, added in f32
+        # TH_GRAD_FP32: each chunk's GEMM writes its bf16 product, which is added to the f32 main_grad
+        # straight away -- the sum over chunks is an f32 accumulation, never a bf16 one.
+        f32_main = mg is not None and mg.dtype != w.dtype
         if f32_main:
             acc = torch.empty(w.shape, device=w.device, dtype=w.dtype)
+            mg_w = mg.view_as(w)
         else:
             acc = mg.view_as(w) if mg is not None else torch.zeros(w.shape, device=w.device, dtype=torch.float32)
         first_acc = mg is not None and (f32_main or not w.th_store.accumulating)
@@ -78,23 +81,26 @@ class _LinearCE(torch.autograd.Function):
             if mg is not None:
                 # dW += dlogitsᵀ hc; with TH_HEAD_WGRAD_NT both operands are transposed first so the
                 # GEMM runs in the K-contiguous form
+                fresh = f32_main or (i == 0 and first_acc)  # overwrite acc instead of accumulating
                 if _HEAD_TN and h2.is_cuda and gemm_tn_supported(w.shape[0], w.shape[1], hc.shape[0]):
                     # TN kernel straight from [tokens, V] logits and [tokens, D] hidden states
-                    gemm_tn_(logits, hc, acc, accumulate=not (i == 0 and first_acc))
-                    continue
-                a_op, b_op = (transpose(logits), transpose(hc).t()) if (_HEAD_NT and h2.is_cuda) else (logits.t(), hc)
-                if i == 0 and first_acc:
-                    torch.mm(a_op, b_op, out=acc)
+                    gemm_tn_(logits, hc, acc, accumulate=not fresh)
                 else:
-                    acc.addmm_(a_op, b_op)
-                del a_op, b_op
+                    a_op, b_op = (transpose(logits), transpose(hc).t()) if (_HEAD_NT and h2.is_cuda) \
+                        else (logits.t(), hc)
+                    if fresh:
+                        torch.mm(a_op, b_op, out=acc)
+                    else:
+                        acc.addmm_(a_op, b_op)
+                    del a_op, b_op
+                if f32_main:
+                    (mg_w.copy_ if (i == 0 and not w.th_store.accumulating) else mg_w.add_)(acc)
             else:
                 acc.addmm_(logits.t().float(), hc.float())
             del logits
         del w_kn
         if f32_main:
-            (mg.add_ if w.th_store.accumulating else mg.copy_)(acc.view_as(mg))
-            del acc
+            del acc, mg_w
         if mg is not None:
             w.th_store.mark_ready(w)
             ctx.gw = None

@@ -97,3 +97,22 @@ def test_tf1_clusterspec_flags(job_as):
     heads = [o.splitlines()[0] for _, o in outs]
     assert heads[0].startswith("[tf1] job=ps:0 address=node-a:2222 ps=1 workers=2 gpus=''")
     assert heads[2].startswith("[tf1] job=worker:1 address=node-b:2224") and heads[2].endswith("gpus='0'")
+
+
+@pytest.mark.parametrize("template,placement", [
+    ("tf2", {"hostname": "node-a", "role": "chief", "gpus": "auto:1"}),
+    ("tf1", {"hostname": "node-a", "role": "worker", "gpuCount": 2}),
+    ("torch", {"hostname": "node-a", "gpus": "auto:2"}),
+    ("torchrun", {"hostname": "node-a", "gpus": "auto"}),       # no count
+    ("torchrun", {"hostname": "node-a", "gpus": "auto:x"}),
+])
+def test_count_placements_are_rejected_outside_torchrun(job_as, template, placement):
+    """ADVICE r2 (job.py:386): device counts are a torchrun-only feature; elsewhere (and for a bare
+    ``auto``) the request is refused with a 4xx instead of pinning GPU 0 or failing with a 500."""
+    st, body = job_as({"template": template, "placements": [placement]})
+    assert 400 <= st < 500, body
+
+
+def test_torchrun_count_placement_is_accepted(job_as):
+    st, body = job_as({"template": "torchrun", "placements": [{"hostname": "node-a", "gpus": "auto:2"}]})
+    assert st == 201 and body["tasks"][0]["fullCommand"].startswith("HIP_VISIBLE_DEVICES=auto:2 ")

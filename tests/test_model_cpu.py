@@ -109,3 +109,31 @@ def test_add_norm_flow_matches_addmm_epilogue_flow_cpu(monkeypatch):
         b = out[False][1][n]
         rel = float((a - b).norm() / (b.norm() + 1e-8))
         assert rel < 3e-2, (n, rel)
+
+
+def test_lm_head_grad_is_f32_accumulated_over_chunks():
+    """ADVICE r2 (cross_entropy.py:67): with an f32 main_grad (TH_GRAD_FP32) the LM-head weight
+    gradient is summed over CE chunks in f32 -- each chunk's bf16 product is added as produced."""
+    import types
+
+    import torch
+
+    from tensorhive_fixed_amd.ops.cross_entropy import linear_cross_entropy
+
+    torch.manual_seed(0)
+    T, D, V, chunk = 512, 64, 96, 16  # 32 chunks: a bf16 running sum would round 32 times
+    h = torch.randn(T, D).bfloat16().requires_grad_()
+    w = (torch.randn(V, D) * 0.05).bfloat16()
+    tgt = torch.randint(0, V, (T,))
+    ready = []
+    w.main_grad = torch.zeros(V * D, dtype=torch.float32)
+    w.th_store = types.SimpleNamespace(accumulating=False, mark_ready=lambda p: ready.append(p))
+    linear_cross_entropy(h, w, tgt, chunk=chunk).backward()
+    assert ready, "the store was told the gradient is final"
+    hd, wd = h.detach().double(), w.double()
+    p = torch.softmax(hd @ wd.t(), -1)
+    p[torch.arange(T), tgt] -= 1
+    ref = (p / T).t() @ hd
+    got = w.main_grad.view(V, D).double()
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err < 4e-3, err  # f32 sum of bf16 chunk products: 2.0e-3; the old bf16 running sum: 6.9e-3

@@ -132,3 +132,66 @@ def test_training_metrics_are_parsed_from_the_task_log(world, client, auth_heade
     assert r.status_code == 200, body
     assert [p["step"] for p in body["series"]] == [10, 20] and body["tokensPerSec"] == 24020.0
     assert client.get(f"/api/tasks/{t.id}/training", headers=auth_headers(users["bob"])).status_code == 403
+
+
+@native
+def test_th_run_pid_history_and_stop_between_runs(tmp_path):
+    """Every incarnation's pid finds the session; a stop landing between a failed run and its
+    restart succeeds (exit 0) and no further run starts (th_run.cpp:443)."""
+    build_all(strict=False)
+    r = _th_run("spawn", "--name", "t4", "--log", str(tmp_path / "t4.log"), "--max-restarts", "5",
+                "--restart-delay", "0.1", "--", "bash", "-c", "sleep 30", state=tmp_path)
+    pids = [int(r.stdout.strip())]
+    for k in (1, 2):  # two crashes -> three incarnations
+        time.sleep(0.3)
+        subprocess.run(["kill", "-9", "--", f"-{pids[-1]}"], check=True)
+        t0 = time.time()
+        while time.time() - t0 < 10 and _status("t4", tmp_path).get("restarts") != k:
+            time.sleep(0.05)
+        pids.append(_status("t4", tmp_path)["pid"])
+    st = _status("t4", tmp_path)
+    assert st["restarts"] == 2 and [int(p) for p in st["pids"].split(",")] == pids
+    # the MIDDLE pid (neither first nor current) still reaches the live run
+    assert _th_run("terminate", "--pid", str(pids[1]), state=tmp_path).returncode == 0
+    assert _th_run("wait", "--name", "t4", "--timeout", "15", state=tmp_path).returncode == 143
+
+    r = _th_run("spawn", "--name", "t5", "--log", str(tmp_path / "t5.log"), "--max-restarts", "5",
+                "--restart-delay", "2", "--", "bash", "-c", "exit 7", state=tmp_path)
+    first = int(r.stdout.strip())
+    t0 = time.time()
+    while time.time() - t0 < 10 and _status("t5", tmp_path).get("status") != "restarting":
+        time.sleep(0.02)
+    assert _th_run("interrupt", "--pid", str(first), state=tmp_path).returncode == 0
+    assert _th_run("wait", "--name", "t5", "--timeout", "15", state=tmp_path).returncode == 7
+    assert _status("t5", tmp_path)["restarts"] == 1  # the pending restart was abandoned, no new run
+
+
+def test_daemon_tracks_a_task_across_several_restarts(world, client, auth_headers):  # noqa: F811
+    """after >= 2 restarts the stored pid must still resolve, the claim must be
+    kept, and a stop must reach the live run -- with and without a sync between the crashes."""
+    from tensorhive_fixed_amd.controllers import task as task_ctl
+
+    d, users, _ = world
+    node = d.transports.get("node-a")
+    j = _job(users["alice"], "auto:2")
+    t = j.tasks[0]
+    t.set_max_restarts(4)
+    assert _execute(d, j.id)[1] == 200
+    t = Job.get(j.id).tasks[0]
+    p1 = t.pid
+    p2 = node.crash_task(p1, code=1)
+    task_ctl.synchronize(t.id)  # the daemon sees the middle incarnation
+    assert Job.get(j.id).tasks[0].pid == p2
+    p3 = node.crash_task(p2, code=1)
+    p4 = node.crash_task(p3, code=1)  # two crashes with no sync between them
+    task_ctl.synchronize(t.id)
+    t = Job.get(j.id).tasks[0]
+    assert t.status is TaskStatus.running and t.pid == p4
+    assert {i for _h, i in GpuAllocation.held()} == {0, 1}
+    r = client.get(f"/api/jobs/{j.id}/stop", query_string={"gracefully": "true"},
+                   headers=auth_headers(users["alice"]))
+    assert r.status_code == 200, r.get_json()
+    assert p4 not in node.sessions  # the stop reached the current run
+    task_ctl.synchronize(t.id)
+    t = Job.get(j.id).tasks[0]
+    assert t.status is TaskStatus.terminated and GpuAllocation.held() == set()

@@ -333,3 +333,31 @@ def test_scaling_harness_efficiency_and_skips():
     eff = {p["n_gpus"]: p["efficiency"] for p in out["points"]}
     assert eff[1] == 1.0 and abs(eff[2] - 49000 / 49400) < 1e-4 and abs(eff[4] - 97500 / 98800) < 1e-4
     assert out["points"][2]["tokens_per_sec_per_gpu"] == 24375.0 and out["points"][1]["zero"] == 1
+
+
+SHELL_CASES = ['"a b"', "/data/*.tfrecord", "$HOME/x", "~/ckpt", "a b", "a;b", '"a;b"', "it's", "--x=1",
+               '{"a": 1}', '{"cluster":{"w":["h:1"]}}', "a\\ b", "x\\", "'quoted already'", "a&&b", "(x)",
+               "tcp://127.0.0.1:29500", "", "{a,b}", 'say "hi there"']
+
+
+def test_shell_value_keeps_one_word_values_and_js_agrees(tmp_path):
+    """ADVICE r2 (orm.py:56): values the shell reads as ONE word are passed verbatim (user quoting,
+    globs, $VARS keep their meaning); splitting values, unbalanced quotes, bare operators and JSON
+    documents are single-quoted.  launch.js renders every case identically."""
+    import shlex as _shlex
+
+    from tensorhive_fixed_amd.models.orm import _shell_value
+
+    expect = {'"a b"': '"a b"', "/data/*.tfrecord": "/data/*.tfrecord", "$HOME/x": "$HOME/x", "a b": "'a b'",
+              "a;b": "'a;b'", '"a;b"': '"a;b"', "it's": "'it'\\''s'", '{"a": 1}': "'{\"a\": 1}'",
+              "'quoted already'": "'quoted already'", "x\\": "'x\\'", "": ""}
+    for v, want in expect.items():
+        assert _shell_value(v) == want, v
+    for v in SHELL_CASES:  # every rendered value is exactly one shell word
+        if v:
+            assert len(_shlex.split(_shell_value(v))) == 1, v
+    out = _node_eval(tmp_path, r"""
+import { shellValue } from "@JS@/launch.js";
+console.log(JSON.stringify(%s.map(shellValue)));
+""" % json.dumps(SHELL_CASES))
+    assert out == [_shell_value(v) for v in SHELL_CASES]
