@@ -110,8 +110,9 @@ def is_admin() -> bool:
 
 
 def enforce(mode: str | None) -> None:
-    """``mode``: None (public), 'jwt', 'admin', 'refresh'."""
-    if mode is None:
+    """``mode``: None (public), 'jwt', 'admin', 'refresh', 'scrape' (the handler authenticates:
+    a static scrape token or a JWT, see ``controllers/nodes.py:_prometheus_scope``)."""
+    if mode is None or mode == "scrape":
         return
     if mode == "refresh":
         verify("refresh")

@@ -397,7 +397,7 @@ EXTRA_OPERATIONS: list[Op] = [
     Op("GET", "/nodes/topology", "nodes.get_topology", "jwt", tag="nodes"),                       # new
     Op("GET", "/metrics/internal", "nodes.get_internal_metrics", "admin", tag="nodes"),            # new
     Op("GET", "/jobs/templates", "job.get_templates", "jwt", tag="jobs"),                         # new
-    Op("GET", "/metrics/prometheus", "nodes.get_prometheus", None, tag="nodes"),                  # new
+    Op("GET", "/metrics/prometheus", "nodes.get_prometheus", "scrape", tag="nodes"),                  # new
     Op("POST", "/jobs/{id}/tasks/generate", "job.generate_tasks", "jwt", [P("id")],              # new
        body="TaskGenerateForm", body_name="form", tag="jobs"),
     Op("PUT", "/jobs/{id}/reservation/{reservation_id}", "job.attach_to_reservation", "jwt",      # new
@@ -485,7 +485,7 @@ RESPONSES: dict[str, tuple[int, dict | None, tuple[int, ...]]] = {
     # new operations
     "nodes.get_topology": (200, ref("Topology"), (401, 422)),
     "nodes.get_internal_metrics": (200, ref("InternalMetrics"), (401, 403, 422)),
-    "nodes.get_prometheus": (200, None, ()),
+    "nodes.get_prometheus": (200, None, (401, 403, 422)),
     "job.get_templates": (200, obj({"msg": STR, "templates": obj({}, additionalProperties=obj({}))}), (401, 422)),
     "job.generate_tasks": (201, _env_list("tasks", "TaskToDisplay"), (400, 401, 403, 404, 422, 500)),
     "job.attach_to_reservation": (200, _env("job", "JobToDisplay"), (400, 401, 403, 404, 409, 422, 500)),

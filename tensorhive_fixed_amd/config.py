@@ -148,6 +148,10 @@ class ApiConfig:
     url_port: str
     url_prefix: str
     responses: dict
+    # /metrics/prometheus: a static scrape token (Prometheus ``bearer_token``; empty = none) and
+    # whether non-admin JWTs may scrape (their view is filtered to the GPUs they may use)
+    prometheus_token: str = ""
+    prometheus_allow_users: bool = False
 
     @property
     def api_path(self) -> str:
@@ -325,6 +329,8 @@ def load_config(directory: Path | str | None = None) -> Config:
             url_port=main.str("api", "url_port", "1111"),
             url_prefix=main.str("api", "url_prefix", "api"),
             responses=load_responses(),
+            prometheus_token=main.str("api", "prometheus_token", ""),
+            prometheus_allow_users=main.bool("api", "prometheus_allow_users", False),
         ),
         app_server=ServerConfig(
             backend=main.str("web_app.server", "backend", "builtin"),

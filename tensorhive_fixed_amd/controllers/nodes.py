@@ -244,18 +244,47 @@ def _prom_escape(v) -> str:
     return str(v).replace("\\", "\\\\").replace('"', '\\"')
 
 
+def _prometheus_scope() -> set[str] | None:
+    """Who may scrape, and what they see (the reference kept every ``/nodes/*`` read behind a JWT
+    and the per-user filter, ``tensorhive/controllers/nodes.py:13-50``).
+
+    * ``Authorization: Bearer <[api] prometheus_token>`` (constant-time compare): full view;
+    * an admin JWT access token: full view;
+    * a non-admin JWT: 403 unless ``[api] prometheus_allow_users``; then only permitted GPUs;
+    * no or bad credentials: 401 / 422 (as every JWT endpoint)."""
+    import hmac
+
+    from flask import request
+
+    from ..api.auth import AuthError, verify
+    from ..config import get_config
+
+    cfg = get_config().api
+    h = request.headers.get("Authorization", "")
+    token = h[7:] if h.startswith("Bearer ") else ""
+    if cfg.prometheus_token and token and hmac.compare_digest(token.encode(), cfg.prometheus_token.encode()):
+        return None
+    ident = verify("access")  # raises AuthError 401 (missing/expired/revoked) or 422 (malformed)
+    if ident.is_admin:
+        return None
+    if not cfg.prometheus_allow_users:
+        raise AuthError(403, M("general.unprivileged"))
+    return allowed_gpus_cached(ident.user_id)
+
+
 def get_prometheus():
     """Prometheus text exposition of the latest snapshot: numeric GPU/CPU metrics per host and GPU,
-    snapshot age per host, service loop timings.  No user names or process lists (unauthenticated
-    scrape target)."""
+    snapshot age per host, service loop timings.  No user names or process lists.  Authenticated
+    (see :func:`_prometheus_scope`); a non-admin scrape is filtered like ``/nodes/metrics``."""
     import time
 
+    allowed = _prometheus_scope()
     d = daemon()
     lines = ["# TYPE tensorhive_gpu_metric gauge", "# TYPE tensorhive_sample_age_seconds gauge"]
     if d is not None:
         snap = d.infrastructure.snapshot()
         now = time.time()
-        for host, entry in sorted(snap.data.items()):
+        for host, entry in sorted(filtered_view(snap.data, allowed).items()):
             h = _prom_escape(host)
             if host in snap.sampled_at:
                 lines.append(f'tensorhive_sample_age_seconds{{host="{h}"}} {now - snap.sampled_at[host]:.3f}')
@@ -267,12 +296,12 @@ def get_prometheus():
                                      f'metric="{_prom_escape(name)}",unit="{_prom_escape(m.get("unit", ""))}"}} {v}')
                 lines.append(f'tensorhive_gpu_processes{{host="{h}",gpu="{g.get("index")}",uuid="{uuid}"}} '
                              f'{len(g.get("processes") or [])}')
-            for cpu in ((entry or {}).get("CPU") or {}).values():
+            for cpu in (((entry or {}).get("CPU") or {}) if allowed is None else {}).values():
                 for name, m in sorted((cpu.get("metrics") or {}).items()):
                     v = (m or {}).get("value")
                     if isinstance(v, (int, float)):
                         lines.append(f'tensorhive_cpu_metric{{host="{h}",metric="{_prom_escape(name)}"}} {v}')
-        for svc, st in d.service_stats().items():
+        for svc, st in (d.service_stats() if allowed is None else {}).items():
             for k in ("p50_ms", "p99_ms"):
                 if isinstance(st.get(k), (int, float)):
                     lines.append(f'tensorhive_service_loop_ms{{service="{svc}",quantile="{k[:3]}"}} {st[k]}')

@@ -45,10 +45,10 @@ def test_reservation_flow(client, new_user, auth_headers, resource1, permissive_
     assert st == 422  # overlap
 
 
-def test_prometheus_exposition(client, daemon):
+def test_prometheus_exposition(client, daemon, new_admin, auth_headers):
     daemon.stub.add_process("node-a", 1, 4242, "someoneprivate")
     daemon.infrastructure.publish("node-a", daemon.stub.sample("node-a"))
-    r = client.get("/api/metrics/prometheus")  # scrape target: no JWT
+    r = client.get("/api/metrics/prometheus", headers=auth_headers(new_admin))
     assert r.status_code == 200 and r.mimetype == "text/plain"
     text = r.get_data(as_text=True)
     assert 'tensorhive_gpu_metric{host="node-a",gpu="0"' in text
@@ -60,6 +60,37 @@ def test_prometheus_exposition(client, daemon):
     for ln in text.splitlines():  # every sample line is `name{labels} number`
         if not ln.startswith("#"):
             float(ln.rsplit(" ", 1)[1])
+
+
+def test_prometheus_scrape_is_authenticated_and_filtered(client, daemon, cfg, new_user, new_admin, auth_headers):
+    """Round-2 verdict weak #8: no anonymous scrape; a static scrape token or an admin JWT sees
+    everything; a non-admin JWT is refused unless allowed, and then sees only permitted GPUs."""
+    import datetime as _dt
+
+    from tensorhive_fixed_amd.models.orm import Resource, Restriction
+    from tensorhive_fixed_amd.core.telemetry import StubBackend
+
+    daemon.infrastructure.publish("node-a", daemon.stub.sample("node-a"))
+    uuids = [StubBackend.gpu_uuid("node-a", i) for i in range(8)]
+    assert client.get("/api/metrics/prometheus").status_code == 401
+    assert client.get("/api/metrics/prometheus", headers={"Authorization": "Bearer nope"}).status_code == 422
+    assert client.get("/api/metrics/prometheus", headers=auth_headers(new_user)).status_code == 403
+    full = client.get("/api/metrics/prometheus", headers=auth_headers(new_admin)).get_data(as_text=True)
+    assert all(u in full for u in uuids) and "tensorhive_cpu_metric" in full
+    cfg.api.prometheus_token = "s3cret-scrape"
+    r = client.get("/api/metrics/prometheus", headers={"Authorization": "Bearer s3cret-scrape"})
+    assert r.status_code == 200 and all(u in r.get_data(as_text=True) for u in uuids)
+    # a restricted user, once allowed: only the GPU their restriction covers
+    cfg.api.prometheus_allow_users = True
+    res = Resource(id=uuids[3], name="MI355X", hostname="node-a")
+    res.save()
+    rs = Restriction(name="gpu3", starts_at=_dt.datetime.utcnow() - _dt.timedelta(hours=1), is_global=False)
+    rs.save()
+    rs.apply_to_user(new_user)
+    rs.apply_to_resource(res)
+    text = client.get("/api/metrics/prometheus", headers=auth_headers(new_user)).get_data(as_text=True)
+    assert uuids[3] in text and not any(u in text for i, u in enumerate(uuids) if i != 3)
+    assert "tensorhive_cpu_metric" not in text and "tensorhive_service_loop_ms" not in text
 
 
 def test_attach_job_to_multi_gpu_reservation(client, daemon, new_user, new_user_2, auth_headers):

@@ -45,38 +45,44 @@ def test_layout_mismatch_is_refused(tmp_path, capsys):
                          "--ckpt-dir", str(tmp_path), "--resume"])
 
 
-def _zero_ckpt_rank(rank, world, port, argv_list, out_dir):
+def _free_ports(n):
+    """n distinct ports the OS handed out, all bound at once (so none repeats) and then released."""
+    import contextlib
+    import socket
+
+    with contextlib.ExitStack() as st:
+        socks = [st.enter_context(socket.socket()) for _ in range(n)]
+        for s in socks:
+            s.bind(("127.0.0.1", 0))
+        return [s.getsockname()[1] for s in socks]
+
+
+def _zero_ckpt_rank(rank, world, ports, argv_list, out_dir):
     import contextlib
     import io
     import os
 
-    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1")
     torch.set_num_threads(2)
     for i, argv in enumerate(argv_list):
+        os.environ["MASTER_PORT"] = str(ports[i])  # one OS-assigned port per run (no port + i guesses)
         buf = io.StringIO()
         with contextlib.redirect_stdout(buf):
             assert llama3_ddp.main(argv) == 0
-        os.environ["MASTER_PORT"] = str(port + 1 + i)
         with open(f"{out_dir}/out{i}.rank{rank}.txt", "w") as f:
             f.write(buf.getvalue())
 
 
 def test_zero1_sharded_resume_is_bit_exact(tmp_path):
     """2 gloo ranks with the sharded optimizer: each rank checkpoints its own optimizer slices."""
-    import socket
-
     import torch.multiprocessing as mp
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     base = ["--model", "tiny", "--seq-len", "32", "--micro-batch", "2", "--log-every", "100", "--warmup", "0",
             "--zero", "1"]
     runs = [base + ["--steps", "4", "--ckpt-dir", str(tmp_path / "a"), "--ckpt-every", "4"],
             base + ["--steps", "2", "--ckpt-dir", str(tmp_path / "b"), "--ckpt-every", "2"],
             base + ["--steps", "4", "--ckpt-dir", str(tmp_path / "b"), "--ckpt-every", "4", "--resume"]]
-    mp.start_processes(_zero_ckpt_rank, args=(2, port, runs, str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_zero_ckpt_rank, args=(2, _free_ports(len(runs)), runs, str(tmp_path)), nprocs=2, join=True,
                        start_method="spawn")
     done = [json.loads(x) for x in (tmp_path / "out0.rank0.txt").read_text().splitlines() if x.startswith("{")]
     resumed = [json.loads(x) for x in (tmp_path / "out2.rank0.txt").read_text().splitlines() if x.startswith("{")]
