@@ -395,7 +395,7 @@ def load_config(directory: Path | str | None = None) -> Config:
         ),
         amd_monitor=AmdMonitorConfig(
             backend=main.str("amd_monitor", "backend", "auto"),
-            probe_enabled=main.bool("amd_monitor", "probe_enabled", False),
+            probe_enabled=main.bool("amd_monitor", "probe_enabled", True),
             probe_period=main.float("amd_monitor", "probe_period", 1.0),
             stub_gpus=main.int("amd_monitor", "stub_gpus", 8),
             counters_enabled=main.bool("amd_monitor", "counters_enabled", False),

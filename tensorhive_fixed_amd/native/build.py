@@ -6,7 +6,9 @@ Targets (all into ``native/bin`` / ``native/lib``; git-ignored, shipped with the
   * ``bin/th-smi``        -- CLI / ``--stream`` agent over the same sampler          [g++ + libamd_smi]
   * ``bin/rccl-bench``    -- RCCL/xGMI collective + direct P2P all-reduce bench      [hipcc + librccl]
   * ``bin/th-counters``   -- device-wide HW counter sampler (rocprofiler-sdk)       [g++ + rocprofiler-sdk]
-The gfx950 kernels (incl. the th-probe kernel) are built by :mod:`..ops.build` into ``libthk.so``.
+  * ``bin/th-probe``      -- per-node probe agent: the gfx950 probe kernel on every GPU [hipcc]
+The gfx950 training kernels (and the same probe kernel, for in-process use) are built by
+:mod:`..ops.build` into ``libthk.so``.
 """
 from __future__ import annotations
 
@@ -24,6 +26,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 CXX = os.environ.get("CXX", "g++")
 HIPCC = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
 ARCH = os.environ.get("TH_OFFLOAD_ARCH", "gfx950")
+KSRC = HERE.parent / "ops" / "csrc"
 
 TARGETS = {
     "th-run": (BIN / "th-run", [CXX, "-O2", "-std=c++17", "-Wall", str(HERE / "th_run.cpp")]),
@@ -35,6 +38,8 @@ TARGETS = {
     "th-counters": (BIN / "th-counters", [CXX, "-O2", "-std=c++17", f"-I{ROCM}/include",
                                           str(HERE / "th_counters.cpp"), f"-L{ROCM}/lib", "-lrocprofiler-sdk",
                                           "-lhsa-runtime64", f"-Wl,-rpath,{ROCM}/lib"]),
+    "th-probe": (BIN / "th-probe", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", f"-I{KSRC}",
+                                    str(HERE / "th_probe.hip")]),
     "rccl-bench": (BIN / "rccl-bench", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}",
                                         str(HERE / "rccl_bench.hip"), f"-L{ROCM}/lib", "-lrccl",
                                         f"-Wl,-rpath,{ROCM}/lib"]),
@@ -49,6 +54,8 @@ for _n in ("th-run", "th-smi"):
     TARGETS[_n + "-asan"] = (_out.with_name(_out.name + "-asan"),
                              [_cmd[0]] + SANITIZE + [c for c in _cmd[1:] if c not in ("-O2", "-O3")])
 SANITIZED = {n for n in TARGETS if n.endswith("-asan")}
+# headers / included sources a target depends on besides the sources on its command line
+DEPS = {"th-probe": [KSRC / "probe.hip", KSRC / "th_common.h"]}
 
 
 def sanitizer_env(report_dir: str) -> dict:
@@ -65,7 +72,7 @@ def path_of(name: str) -> Path:
 
 def _build_one(name: str, force: bool) -> tuple[str, str | None]:
     out, cmd = TARGETS[name]
-    srcs = [Path(c) for c in cmd if c.endswith((".cpp", ".hip"))]
+    srcs = [Path(c) for c in cmd if c.endswith((".cpp", ".hip"))] + DEPS.get(name.replace("-asan", ""), [])
     if not force and out.exists() and all(out.stat().st_mtime >= s.stat().st_mtime for s in srcs):
         return name, None
     if shutil.which(cmd[0]) is None and not Path(cmd[0]).exists():

@@ -68,6 +68,12 @@ double hbm_gbps_per_acc() {
 std::mutex g_mu;
 bool g_init = false;
 std::vector<Gpu> g_gpus;
+// The monitor's own processes (this process, the th-probe agent, th-counters, ...) are never
+// tenants: they are dropped from every process list (reference: InfrastructureManager.py:57,70-76
+// filtered its own non-tenant commands).  Set with thsmi_set_ignored_pids / th-smi --ignore-pid.
+std::set<long> g_ignored;
+
+bool ignored_pid(long pid) { return pid == (long)getpid() || g_ignored.count(pid) > 0; }
 unsigned long long g_cpu_prev_total = 0, g_cpu_prev_idle = 0;
 
 uint64_t now_ns() {
@@ -407,6 +413,7 @@ std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd,
   std::string ps = "[";
   bool first = true;
   for (const auto& p : procs) {
+    if (ignored_pid(p.first)) continue;
     ProcInfo pi = resolve_pid(p.first);
     if (pi.uid < 0 && pi.cmd.empty()) continue;  // exited between the two reads
     if (!first) ps += ",";
@@ -453,8 +460,19 @@ extern "C" int thsmi_sample_json(char* buf, int cap) {
   auto drm = drm_processes();
   std::string s = "{\"ts_ns\":" + std::to_string(ts) + ",\"cpu\":" + cpu_json() + ",\"gpus\":[";
   for (size_t i = 0; i < g_gpus.size(); ++i) s += (i ? "," : "") + gpu_json(g_gpus[i], kfd, drm, ts);
+  s += "],\"ignored_pids\":[" + std::to_string((long)getpid());
+  for (long p : g_ignored) s += "," + std::to_string(p);
   s += "]}";
   return emit(s, buf, cap);
+}
+
+// Replace the ignore list (pids of the monitor's own helper processes); returns its size.
+extern "C" int thsmi_set_ignored_pids(const long* pids, int n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_ignored.clear();
+  for (int i = 0; i < n; ++i)
+    if (pids[i] > 0) g_ignored.insert(pids[i]);
+  return (int)g_ignored.size();
 }
 
 extern "C" int thsmi_topology_json(char* buf, int cap) {
@@ -483,14 +501,17 @@ extern "C" int thsmi_topology_json(char* buf, int cap) {
 int main(int argc, char** argv) {
   int stream_ms = -1;
   bool topo = false;
+  std::vector<long> ignore;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--stream") && i + 1 < argc) stream_ms = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--topology")) topo = true;
+    else if (!strcmp(argv[i], "--ignore-pid") && i + 1 < argc) ignore.push_back(atol(argv[++i]));
   }
   if (thsmi_init() < 0) {
     fprintf(stderr, "th-smi: amdsmi init failed\n");
     return 1;
   }
+  thsmi_set_ignored_pids(ignore.data(), (int)ignore.size());
   std::vector<char> buf(1 << 20);
   auto once = [&](bool t) {
     int n = t ? thsmi_topology_json(buf.data(), (int)buf.size()) : thsmi_sample_json(buf.data(), (int)buf.size());

@@ -9,6 +9,10 @@
 // The host compares against an idle-device baseline: mfma_busy ~ 1 - t_idle/t_now and
 // hbm_bw_share ~ 1 - bw_now/bw_idle.  A probe costs tens of microseconds; at one probe per
 // second the device-time budget is < 0.01 %.
+//
+// State is per HIP device (th_probe_init/launch/collect take the device index), so one process
+// probes every GPU of a node: the `th-probe` agent (native/th_probe.hip) does exactly that, out of
+// the daemon's process, and streams one JSON line per period.
 #include "th_common.h"
 
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
@@ -78,42 +82,76 @@ struct ProbeState {
   float last_latency_us = 0.f;  // launch-to-completion of the last probe, incl. waiting for a free CU
   int max_wg = 0;
   long per_wg_vec = 0;
+  int pending_wg = 0;  // workgroups of a launched, not yet collected probe
 };
-ProbeState g_probe;
+constexpr int kMaxDevices = 64;
+// One independent state per HIP device: every GPU of a node is probed by one process, each on
+// its own non-blocking stream (round-2 verdict: the probe used to cover device 0 only).
+ProbeState g_probe[kMaxDevices];
+
+ProbeState* state_of(int device) {
+  if (device < 0 || device >= kMaxDevices || g_probe[device].device != device) return nullptr;
+  return &g_probe[device];
+}
 }  // namespace
 
 // Allocate the probe's buffers on `device`: `slice_kb` KB of HBM per workgroup, up to `max_wg`.
+// Leaves the calling thread's current device unchanged.
 extern "C" int th_probe_init(int device, int max_wg, int slice_kb) {
-  if (g_probe.device >= 0) return 0;
+  if (device < 0 || device >= kMaxDevices || max_wg <= 0 || slice_kb <= 0) return -1;
+  ProbeState& st = g_probe[device];
+  if (st.device == device) return 0;
+  int prev = 0;
+  hipGetDevice(&prev);
   if (hipSetDevice(device) != hipSuccess) return 1;
-  g_probe.max_wg = max_wg;
-  g_probe.per_wg_vec = (long)slice_kb * 1024 / 16;
-  if (hipStreamCreateWithFlags(&g_probe.stream, hipStreamNonBlocking) != hipSuccess) return 2;
-  if (hipMalloc((void**)&g_probe.hbm, (size_t)max_wg * g_probe.per_wg_vec * 16) != hipSuccess) return 3;
-  hipMemsetAsync(g_probe.hbm, 0, (size_t)max_wg * g_probe.per_wg_vec * 16, g_probe.stream);
-  if (hipMalloc((void**)&g_probe.sink, 64) != hipSuccess) return 4;
-  if (hipHostMalloc((void**)&g_probe.host, (size_t)max_wg * 4 * 8, hipHostMallocMapped) != hipSuccess) return 5;
-  if (hipEventCreate(&g_probe.ev0) != hipSuccess || hipEventCreate(&g_probe.ev1) != hipSuccess) return 6;
-  hipStreamSynchronize(g_probe.stream);
-  g_probe.device = device;
+  int rc = 0;
+  st.max_wg = max_wg;
+  st.per_wg_vec = (long)slice_kb * 1024 / 16;
+  const size_t bytes = (size_t)max_wg * st.per_wg_vec * 16;
+  if (hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking) != hipSuccess) rc = 2;
+  else if (hipMalloc((void**)&st.hbm, bytes) != hipSuccess) rc = 3;
+  else if (hipMemsetAsync(st.hbm, 0, bytes, st.stream) != hipSuccess) rc = 3;
+  else if (hipMalloc((void**)&st.sink, 64) != hipSuccess) rc = 4;
+  else if (hipHostMalloc((void**)&st.host, (size_t)max_wg * 4 * 8, hipHostMallocMapped) != hipSuccess) rc = 5;
+  else if (hipEventCreate(&st.ev0) != hipSuccess || hipEventCreate(&st.ev1) != hipSuccess) rc = 6;
+  else if (hipStreamSynchronize(st.stream) != hipSuccess) rc = 7;
+  if (rc == 0) st.device = device;
+  hipSetDevice(prev);
+  return rc;
+}
+
+// Launch one probe on `device` without waiting (so every GPU of a node is probed at the same
+// moment); th_probe_collect() waits for it and decodes the result.
+extern "C" int th_probe_launch(int device, int n_wg, int mfma_iters) {
+  ProbeState* st = state_of(device);
+  if (!st || n_wg <= 0 || n_wg > st->max_wg || mfma_iters <= 0) return -1;
+  unsigned long long* dev_host = nullptr;
+  if (hipHostGetDevicePointer((void**)&dev_host, st->host, 0) != hipSuccess) return 2;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(device);
+  hipEventRecord(st->ev0, st->stream);
+  th_probe_kernel<<<n_wg, 256, 0, st->stream>>>(st->hbm, st->per_wg_vec, mfma_iters, dev_host, st->sink);
+  const hipError_t e = hipGetLastError();
+  hipEventRecord(st->ev1, st->stream);
+  hipSetDevice(prev);
+  if (e != hipSuccess) return 3;
+  st->pending_wg = n_wg;
   return 0;
 }
 
-// Run one probe; out[5*i..] = {xcc_id, mfma_us, hbm_us, hbm_GBps, bytes} for workgroup i.
-extern "C" int th_probe_sample(int n_wg, int mfma_iters, double* out) {
-  if (g_probe.device < 0 || n_wg <= 0 || n_wg > g_probe.max_wg) return -1;
-  unsigned long long* dev_host = nullptr;
-  if (hipHostGetDevicePointer((void**)&dev_host, g_probe.host, 0) != hipSuccess) return 2;
-  hipEventRecord(g_probe.ev0, g_probe.stream);
-  th_probe_kernel<<<n_wg, 256, 0, g_probe.stream>>>(g_probe.hbm, g_probe.per_wg_vec, mfma_iters, dev_host,
-                                                    g_probe.sink);
-  if (hipGetLastError() != hipSuccess) return 3;
-  hipEventRecord(g_probe.ev1, g_probe.stream);
-  if (hipStreamSynchronize(g_probe.stream) != hipSuccess) return 4;
+// Wait for the launched probe; out[5*i..] = {xcc_id, mfma_us, hbm_us, hbm_GBps, bytes} for
+// workgroup i.  Returns the number of workgroups.
+extern "C" int th_probe_collect(int device, double* out) {
+  ProbeState* st = state_of(device);
+  if (!st || st->pending_wg <= 0) return -1;
+  const int n_wg = st->pending_wg;
+  st->pending_wg = 0;
+  if (hipStreamSynchronize(st->stream) != hipSuccess) return -4;
   float ms = 0.f;
-  g_probe.last_latency_us = hipEventElapsedTime(&ms, g_probe.ev0, g_probe.ev1) == hipSuccess ? ms * 1e3f : 0.f;
+  st->last_latency_us = hipEventElapsedTime(&ms, st->ev0, st->ev1) == hipSuccess ? ms * 1e3f : 0.f;
   for (int i = 0; i < n_wg; ++i) {
-    const unsigned long long* r = g_probe.host + 4 * i;
+    const unsigned long long* r = st->host + 4 * i;
     const double mfma_us = r[1] / 100.0, hbm_us = r[2] / 100.0;  // 100 MHz ticks
     out[5 * i + 0] = (double)r[0];
     out[5 * i + 1] = mfma_us;
@@ -124,19 +162,35 @@ extern "C" int th_probe_sample(int n_wg, int mfma_iters, double* out) {
   return n_wg;
 }
 
-// Queue-to-completion time of the last probe (us).  A tenant kernel that holds every CU's register
-// file (e.g. a 1-wave/SIMD MFMA GEMM) never shares a SIMD with the probe, so it does not slow the
-// probe's MFMA chain; it delays the probe's dispatch instead -- this latency is what rises.
-extern "C" double th_probe_last_latency_us(void) { return (double)g_probe.last_latency_us; }
+// Launch + collect on one device.
+extern "C" int th_probe_sample(int device, int n_wg, int mfma_iters, double* out) {
+  const int rc = th_probe_launch(device, n_wg, mfma_iters);
+  if (rc != 0) return rc < 0 ? rc : -rc;
+  return th_probe_collect(device, out);
+}
 
-extern "C" int th_probe_shutdown(void) {
-  if (g_probe.device < 0) return 0;
-  hipEventDestroy(g_probe.ev0);
-  hipEventDestroy(g_probe.ev1);
-  hipFree(g_probe.hbm);
-  hipFree(g_probe.sink);
-  hipHostFree(g_probe.host);
-  hipStreamDestroy(g_probe.stream);
-  g_probe = ProbeState();
+// Queue-to-completion time of the last probe on `device` (us).  A tenant kernel that holds every
+// CU's register file (e.g. a 1-wave/SIMD MFMA GEMM) never shares a SIMD with the probe, so it does
+// not slow the probe's MFMA chain; it delays the probe's dispatch instead -- this latency rises.
+extern "C" double th_probe_last_latency_us(int device) {
+  ProbeState* st = state_of(device);
+  return st ? (double)st->last_latency_us : -1.0;
+}
+
+extern "C" int th_probe_shutdown(int device) {
+  ProbeState* st = state_of(device);
+  if (!st) return 0;
+  int prev = 0;
+  hipGetDevice(&prev);
+  hipSetDevice(device);
+  hipStreamSynchronize(st->stream);
+  hipEventDestroy(st->ev0);
+  hipEventDestroy(st->ev1);
+  hipFree(st->hbm);
+  hipFree(st->sink);
+  hipHostFree(st->host);
+  hipStreamDestroy(st->stream);
+  hipSetDevice(prev);
+  *st = ProbeState();
   return 0;
 }
