@@ -70,18 +70,19 @@ def main() -> int:
     from tensorhive_fixed_amd.models.llama3 import LlamaConfig
     from tensorhive_fixed_amd.ops import _lib
     from tensorhive_fixed_amd.ops.attention import attention_backend
-    from tensorhive_fixed_amd.parallel.dist import barrier, init_distributed, shutdown
+    from tensorhive_fixed_amd.parallel.dist import barrier, init_distributed, rank_census, shutdown
     from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer, run_timed
 
+    info = init_distributed()  # binds this rank to its GPU's NUMA CPUs before HIP starts any thread
     if torch.cuda.is_available():
         _lib.load(build_if_missing=True)  # the HIP kernels must be what runs; fail loudly otherwise
-    info = init_distributed()
     if info.world != args.gpus and info.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {info.world}", file=sys.stderr)
     cfg = LlamaConfig.named(args.model)
     tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb,
                  zero=args.zero)
     res = run_timed(tr, args.steps, args.warmup)
+    census = rank_census(info)  # collective: every rank takes part, after the timed region
     n = info.world
     flops = cfg.flops_per_token(args.seq_len) * res["tokens_per_sec"]
     line = {
@@ -114,6 +115,7 @@ def main() -> int:
         "tflops_per_gpu": round(flops / n / 1e12, 1),
         "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
         "final_loss": round(res["loss"], 4),
+        "dist": census,
     }
     if info.is_main:
         line["daemon"] = daemon_poll_latency() if args.daemon_bench else None

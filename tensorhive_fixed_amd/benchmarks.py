@@ -476,14 +476,18 @@ def multitenant(jobs_per_user: int = 8, seed: int = 0, duration_s: tuple[float, 
                         f"{duration_s[0]}-{duration_s[1]} s, mean inter-arrival {arrival_s} s"}
 
 
-def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3) -> dict:
+def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3, bucket_mb: float | None = None,
+                     extra: list[str] | None = None) -> dict:
     """Run bench.py (torchrun for gpus>1) and return its JSON line."""
+    args = ["--gpus", str(gpus), "--steps", str(steps), "--warmup", str(warmup)]
+    if bucket_mb is not None:
+        args += ["--bucket-mb", f"{bucket_mb:g}"]
+    args += list(extra or [])
     if gpus > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-               "--master-addr", "127.0.0.1", "--master-port", "29511", str(ROOT / "bench.py"),
-               "--gpus", str(gpus), "--steps", str(steps), "--warmup", str(warmup)]
+               "--master-addr", "127.0.0.1", "--master-port", "29511", str(ROOT / "bench.py")] + args
     else:
-        cmd = [sys.executable, str(ROOT / "bench.py"), "--steps", str(steps), "--warmup", str(warmup)]
+        cmd = [sys.executable, str(ROOT / "bench.py")] + args
     r = subprocess.run(cmd, capture_output=True, text=True)
     for line in reversed(r.stdout.splitlines()):
         if line.startswith("{"):
@@ -492,10 +496,47 @@ def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3) -> dict:
 
 
 def scaling(gpu_counts: list[int] | None = None, steps: int = 10, warmup: int = 3,
-            run=None, available: int | None = None) -> dict:
+            run=None, available: int | None = None, bucket_mbs: list[float] | None = None) -> dict:
     """Weak-scaling curve of the training payload on one node (N08 c): ``bench.py`` at each GPU
     count (torchrun, one rank per GPU, RCCL), the per-N whole-job tokens/s and the efficiency
-    ``tokens_per_sec(N) / (N * tokens_per_sec(1))``.  Counts above the node's GPUs are skipped."""
+    ``tokens_per_sec(N) / (N * tokens_per_sec(1))``.  Counts above the node's GPUs are skipped.
+
+    ``bucket_mbs`` sweeps the gradient bucket size: every multi-GPU count runs once per size (the
+    1-GPU point has no collectives and runs once); each point records its size, the best size per
+    count is reported in ``best_bucket_mb``.  Each point also keeps the run's rank census
+    (``dist``: world size, distinct GPUs, NUMA binding) so the curve is self-verifying."""
+    if bucket_mbs:
+        sweep = [float(b) for b in bucket_mbs]
+        base_run = run or (lambda n, b: train_throughput(n, steps, warmup, bucket_mb=b))
+        out = None
+        single: dict = {}  # the 1-GPU point has no collectives: measured once, reused by every size
+
+        def run_one(n, b):
+            if n == 1:
+                if "doc" not in single:
+                    single["doc"] = base_run(1, b)
+                return single["doc"]
+            return base_run(n, b)
+
+        for b in sweep:
+            part = scaling(gpu_counts, steps, warmup, run=lambda n, b=b: run_one(n, b), available=available)
+            for p in part["points"]:
+                p["bucket_mb"] = b
+            if out is None:
+                out = part
+            else:  # the 1-GPU baseline is measured once; later sweeps add only multi-GPU points
+                base = out["points"][0]["tokens_per_sec"]
+                for p in part["points"]:
+                    if p["n_gpus"] > 1:
+                        p["efficiency"] = round(p["tokens_per_sec"] / (p["n_gpus"] * base), 4)
+                        out["points"].append(p)
+        best: dict = {}
+        for p in out["points"]:
+            if p["n_gpus"] > 1 and (p["n_gpus"] not in best or p["tokens_per_sec"] > best[p["n_gpus"]][1]):
+                best[p["n_gpus"]] = (p["bucket_mb"], p["tokens_per_sec"])
+        out["best_bucket_mb"] = {str(n): b for n, (b, _v) in sorted(best.items())}
+        out["bucket_sweep_mb"] = sweep
+        return out
     if available is None:
         import torch
 
@@ -511,9 +552,11 @@ def scaling(gpu_counts: list[int] | None = None, steps: int = 10, warmup: int = 
         v = float(doc["value"])
         if n == 1:
             base = v
+        census = doc.get("dist") or {}
         points.append({"n_gpus": n, "tokens_per_sec": v, "ms_per_step": doc.get("ms_per_step"),
                        "tokens_per_sec_per_gpu": round(v / n, 1),
                        "efficiency": round(v / (n * base), 4) if base else None,
-                       "zero": (doc.get("config") or {}).get("zero")})
+                       "zero": (doc.get("config") or {}).get("zero"),
+                       "world_size": census.get("world_size"), "distinct_devices": census.get("distinct_devices")})
     return {"metric": "llama3_8b_bf16_ddp_train_tokens_per_sec", "scaling": "weak", "points": points,
             "skipped": [n for n in (gpu_counts or [1, 2, 4, 8]) if n not in counts]}

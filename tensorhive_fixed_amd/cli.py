@@ -218,7 +218,9 @@ def doctor():
 @click.option("--requests", default=1000)
 @click.option("--gpus", default=1)
 @click.option("--pinned", is_flag=True, help="multitenant: reference-style pinned device pairs")
-def bench(what, requests, gpus, pinned):
+@click.option("--bucket-mb", "bucket_mb", multiple=True, type=float,
+              help="scaling: gradient bucket sizes to sweep (repeat the option); train: the bucket size")
+def bench(what, requests, gpus, pinned, bucket_mb):
     """Benchmarks of BASELINE.md: poll latency, queued-job launch latency, multi-tenant queue
     wait / GPU utilisation, training tokens/s, and its 1/2/4/8-GPU weak-scaling curve."""
     from . import benchmarks
@@ -232,9 +234,9 @@ def bench(what, requests, gpus, pinned):
     elif what == "scheduled":
         click.echo(json.dumps(benchmarks.scheduled_training(gpus)))
     elif what == "scaling":  # 1, 2, 4, 8 GPUs (those the node has), weak-scaling efficiency
-        click.echo(json.dumps(benchmarks.scaling([1, 2, 4, 8])))
+        click.echo(json.dumps(benchmarks.scaling([1, 2, 4, 8], bucket_mbs=list(bucket_mb) or None)))
     else:
-        click.echo(json.dumps(benchmarks.train_throughput(gpus)))
+        click.echo(json.dumps(benchmarks.train_throughput(gpus, bucket_mb=bucket_mb[0] if bucket_mb else None)))
 
 
 def rocprof_prefix(task_id: int, pmc: str = "") -> str:

@@ -245,6 +245,14 @@ class LauncherConfig:
     master_port: int
     bucket_mb: int
     restart_delay: float = 5.0  # seconds between a failed run and its restart (task maxRestarts)
+    # rank CPU binding (parallel/affinity.py): numa | exclusive | none
+    cpu_bind: str = "numa"
+    # RCCL knobs written into the torchrun template (empty = RCCL's own choice); bench.py records
+    # the effective values in its JSON line
+    rccl_min_nchannels: str = ""
+    rccl_max_nchannels: str = ""
+    rccl_algo: str = ""
+    rccl_proto: str = ""
 
 
 @dataclass
@@ -408,6 +416,11 @@ def load_config(directory: Path | str | None = None) -> Config:
             master_port=main.int("launcher", "master_port", 29500),
             bucket_mb=main.int("launcher", "bucket_mb", 256),
             restart_delay=main.float("launcher", "restart_delay", 5.0),
+            cpu_bind=main.str("launcher", "cpu_bind", "numa"),
+            rccl_min_nchannels=main.str("launcher", "rccl_min_nchannels", ""),
+            rccl_max_nchannels=main.str("launcher", "rccl_max_nchannels", ""),
+            rccl_algo=main.str("launcher", "rccl_algo", ""),
+            rccl_proto=main.str("launcher", "rccl_proto", ""),
         ),
     )
 

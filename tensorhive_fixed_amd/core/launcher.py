@@ -16,7 +16,6 @@ Here the server owns the launch recipe:
 from __future__ import annotations
 
 import json
-from pathlib import Path
 
 RCCL_ENV = {
     "HSA_ENABLE_IPC_MODE_LEGACY": "0",
@@ -76,9 +75,25 @@ def order_for_rings(indices: list[int], topology: dict | None) -> list[int]:
     return sorted(indices, key=lambda i: (info.get(i, {}).get("numa_node", 0), i))
 
 
-def cpu_list_for_numa(node: int) -> str | None:
-    p = Path(f"/sys/devices/system/node/node{node}/cpulist")
-    return p.read_text().strip() if p.exists() else None
+def rccl_env(cfg=None) -> dict[str, str]:
+    """The environment a torchrun task starts with: the fixed RCCL/HIP presets, the rank CPU
+    binding mode (applied by every rank itself, ``parallel/affinity.py``) and the RCCL channel /
+    algorithm knobs of ``[launcher]`` that are set."""
+    env = dict(RCCL_ENV)
+    if cfg is None:
+        try:
+            from ..config import get_config
+
+            cfg = get_config().launcher
+        except Exception:  # noqa: BLE001 -- no config installed (library use)
+            cfg = None
+    env["TH_CPU_BIND"] = getattr(cfg, "cpu_bind", "numa") or "numa"
+    for key, var in (("rccl_min_nchannels", "NCCL_MIN_NCHANNELS"), ("rccl_max_nchannels", "NCCL_MAX_NCHANNELS"),
+                     ("rccl_algo", "NCCL_ALGO"), ("rccl_proto", "NCCL_PROTO")):
+        v = str(getattr(cfg, key, "") or "").strip()
+        if v:
+            env[var] = v
+    return env
 
 
 def hip_visible_devices(indices: list[int]) -> str:
@@ -97,7 +112,7 @@ def torchrun_task(host: str, gpu_indices: list[int] | int, master_host: str, mas
     else:
         devices, n = hip_visible_devices(gpu_indices), len(gpu_indices)
     envs = [{"name": "HIP_VISIBLE_DEVICES", "value": devices}]
-    envs += [{"name": k, "value": v} for k, v in RCCL_ENV.items()]
+    envs += [{"name": k, "value": v} for k, v in rccl_env().items()]
     params = [{"name": "--nnodes=", "value": str(nnodes)},
               {"name": "--nproc_per_node=", "value": str(n)},
               {"name": "--rdzv_backend=", "value": "c10d"},

@@ -7,7 +7,7 @@ on ROCm, running over xGMI inside an MI355X node -- or ``gloo`` for CPU runs/tes
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -20,6 +20,7 @@ class DistInfo:
     world: int
     device: torch.device
     backend: str | None
+    affinity: dict = field(default_factory=dict)  # parallel/affinity.py plan + whether it was applied
 
     @property
     def is_main(self) -> bool:
@@ -41,6 +42,15 @@ def apply_env_defaults() -> None:
         os.environ.setdefault(k, v)
 
 
+COMM_ENV_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_ENABLE_IPC", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                     "TH_CPU_BIND", "GPU_MAX_HW_QUEUES")
+
+
+def comm_env() -> dict[str, str]:
+    """The communication-relevant environment this rank actually runs with (recorded by bench.py)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(COMM_ENV_PREFIXES)}
+
+
 def forced_collectives() -> bool:
     """TH_FORCE_COLLECTIVES=1: a one-rank run still creates the process group and issues every
     collective (and the sharded optimizer), so the RCCL path can be tested on a one-GPU box."""
@@ -53,6 +63,15 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU binding first: nothing below may have created threads or touched the GPU yet.  Counting
+    # devices here would initialise HIP, so the affinity code reads the KFD topology from sysfs.
+    from .affinity import bind
+
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    try:
+        aff = bind(local_rank, local_world)
+    except OSError as e:  # a restricted sysfs / cpuset: run unbound rather than fail
+        aff = {"applied": False, "reason": str(e)}
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
@@ -71,7 +90,41 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     elif dist.is_initialized():
         backend = dist.get_backend()
-    return DistInfo(rank, local_rank, world, device, backend)
+    return DistInfo(rank, local_rank, world, device, backend, aff)
+
+
+def device_bdf(device: torch.device) -> str | None:
+    """PCI BDF of a GPU as HIP reports it (None on CPU)."""
+    if device.type != "cuda":
+        return None
+    p = torch.cuda.get_device_properties(device)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+def rank_census(info: DistInfo) -> dict:
+    """Self-verification record of a distributed run, all-gathered from every rank: the world the
+    process group really formed, each rank's GPU (PCI BDF), NUMA node and CPU binding, and the
+    communication environment.  ``distinct_devices == world_size`` proves the communicator
+    spans that many different GPUs (round-2 verdict item 2)."""
+    import socket
+
+    from .affinity import current_affinity
+
+    bdf = device_bdf(info.device)
+    mine = {"rank": info.rank, "local_rank": info.local_rank, "host": socket.gethostname(),
+            "bdf": bdf, "numa_node": info.affinity.get("numa_node"),
+            "cpus": current_affinity(), "bound": bool(info.affinity.get("applied"))}
+    if bdf and info.affinity.get("bdf") and info.affinity["bdf"] != bdf:
+        mine["affinity_bdf_mismatch"] = info.affinity["bdf"]  # sysfs order disagreed with HIP's
+    if dist.is_initialized():
+        ranks: list = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, mine)
+        world, backend = dist.get_world_size(), dist.get_backend()
+    else:
+        ranks, world, backend = [mine], 1, None
+    devices = {(r["host"], r["bdf"]) for r in ranks if r["bdf"]}
+    return {"world_size": world, "backend": backend, "distinct_devices": len(devices), "ranks": ranks,
+            "comm_env": comm_env()}
 
 
 def barrier(info: DistInfo) -> None:

@@ -39,3 +39,11 @@ def test_multi_rank_bench_prints_one_json_line(tmp_path, world):
     assert d["config"]["zero"] == 1  # sharded optimizer is the multi-rank default
     # whole-job aggregate: tokens of both ranks over the (max-over-ranks) step time
     assert abs(d["value"] - world * 2 * 64 / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
+    # self-verification (round-2 verdict item 2): the process group the ranks really formed
+    census = d["dist"]
+    assert census["world_size"] == world and census["backend"] == "gloo"
+    assert [r["rank"] for r in census["ranks"]] == list(range(world))
+    assert sorted(r["local_rank"] for r in census["ranks"]) == list(range(world))
+    assert all(r["cpus"] for r in census["ranks"]) and "bound" in census["ranks"][0]
+    assert census["comm_env"].get("TORCH_NCCL_ASYNC_ERROR_HANDLING") == "1"
+    assert census["distinct_devices"] == 0  # CPU ranks have no GPU; on MI355X it must equal world_size

@@ -335,6 +335,25 @@ def test_scaling_harness_efficiency_and_skips():
     assert out["points"][2]["tokens_per_sec_per_gpu"] == 24375.0 and out["points"][1]["zero"] == 1
 
 
+def test_scaling_bucket_sweep_records_each_size_and_the_best():
+    from tensorhive_fixed_amd import benchmarks
+
+    calls = []
+
+    def run(n, b):
+        calls.append((n, b))
+        v = 24700.0 * n * (1.0 if n == 1 else (0.97 if b == 256 else 0.93))
+        return {"value": v, "ms_per_step": 1000.0, "config": {"zero": int(n > 1)},
+                "dist": {"world_size": n, "distinct_devices": n}}
+
+    out = benchmarks.scaling([1, 2, 8], available=8, run=run, bucket_mbs=[64, 256])
+    assert calls.count((1, 64)) == 1 and (1, 256) not in calls  # the 1-GPU point runs once
+    assert sorted((p["n_gpus"], p["bucket_mb"]) for p in out["points"]) == [(1, 64), (2, 64), (2, 256), (8, 64), (8, 256)]
+    assert out["best_bucket_mb"] == {"2": 256.0, "8": 256.0} and out["bucket_sweep_mb"] == [64.0, 256.0]
+    p8 = next(p for p in out["points"] if p["n_gpus"] == 8 and p["bucket_mb"] == 256)
+    assert p8["efficiency"] == 0.97 and p8["distinct_devices"] == 8 and p8["world_size"] == 8
+
+
 SHELL_CASES = ['"a b"', "/data/*.tfrecord", "$HOME/x", "~/ckpt", "a b", "a;b", '"a;b"', "it's", "--x=1",
                '{"a": 1}', '{"cluster":{"w":["h:1"]}}', "a\\ b", "x\\", "'quoted already'", "a&&b", "(x)",
                "tcp://127.0.0.1:29500", "", "{a,b}", 'say "hi there"']
