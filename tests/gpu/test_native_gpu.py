@@ -181,3 +181,16 @@ def test_direct_allreduce_matches_host_sum_with_virtual_peers():
                            capture_output=True, text=True, timeout=120)
         doc = json.loads(r.stdout.strip().splitlines()[-1])
         assert r.returncode == 0 and doc["ok"] and doc["mismatches"] == 0, (r.stdout, r.stderr)
+
+
+def test_rccl_bench_both_modes_on_one_gpu():
+    """N06: the single-process (ncclCommInitAll) and one-rank-per-GPU (torchrun + ncclCommInitRank)
+    modes both run and print output that matches the pinned schema (core/rccl_bench.py)."""
+    from tensorhive_fixed_amd.core import rccl_bench
+
+    single = rccl_bench.run_single(gpus=1, min_bytes=1 << 20, max_bytes=4 << 20, iters=5, direct=True)
+    assert single["header"]["mode"] == "single_process" and single["header"]["world"] == 1
+    assert {r["op"] for r in single["results"]} == {"allreduce", "reducescatter", "allgather"}
+    ranked = rccl_bench.run_per_rank(1, min_bytes=1 << 20, max_bytes=4 << 20, iters=5)
+    assert ranked["header"]["mode"] == "per_rank" and ranked["header"]["rccl_version"] > 0
+    assert len(ranked["results"]) == 3 * 3 and all(r["gpus"] == 1 for r in ranked["results"])
