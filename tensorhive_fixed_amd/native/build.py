@@ -46,14 +46,25 @@ TARGETS = {
 }
 
 
-# ASan + UBSan builds of the host tools (``th-run-asan``, ``th-smi-asan``): built on demand by the
-# sanitizer tests, never shipped.  Host code only -- GPU sanitizers are not used on this pool.
+# libthsmi's multi-threaded stress driver (built only for the sanitizer runs below)
+_STRESS = [CXX, "-O2", "-std=c++17", "-pthread", f"-I{ROCM}/include", str(HERE / "thsmi.cpp"),
+           str(HERE / "thsmi_stress.cpp"), f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib"]
+
+# Sanitizer builds of the host tools, built on demand by the sanitizer tests, never shipped.  Host
+# code only -- GPU sanitizers are not used on this pool.
+#   *-asan: AddressSanitizer + UBSan (th-run, th-smi, thsmi-stress)
+#   *-tsan: ThreadSanitizer (th-run's forked monitor, libthsmi under 4 threads, the th-counters
+#           reader with rocprofiler-sdk's own threads)
 SANITIZE = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
-for _n in ("th-run", "th-smi"):
-    _out, _cmd = TARGETS[_n]
-    TARGETS[_n + "-asan"] = (_out.with_name(_out.name + "-asan"),
-                             [_cmd[0]] + SANITIZE + [c for c in _cmd[1:] if c not in ("-O2", "-O3")])
-SANITIZED = {n for n in TARGETS if n.endswith("-asan")}
+SANITIZE_THREAD = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=thread"]
+for _n, _cmd0, _kinds in (("th-run", None, ("asan", "tsan")), ("th-smi", None, ("asan", "tsan")),
+                          ("thsmi-stress", _STRESS, ("asan", "tsan")), ("th-counters", None, ("tsan",))):
+    _out, _cmd = (BIN / _n, _cmd0) if _cmd0 else TARGETS[_n]
+    for _k in _kinds:
+        _flags = SANITIZE if _k == "asan" else SANITIZE_THREAD
+        TARGETS[f"{_n}-{_k}"] = (_out.with_name(f"{_out.name}-{_k}"),
+                                 [_cmd[0]] + _flags + [c for c in _cmd[1:] if c not in ("-O2", "-O3")])
+SANITIZED = {n for n in TARGETS if n.endswith(("-asan", "-tsan"))}
 # headers / included sources a target depends on besides the sources on its command line
 DEPS = {"th-probe": [KSRC / "probe.hip", KSRC / "th_common.h"]}
 
@@ -66,13 +77,19 @@ def sanitizer_env(report_dir: str) -> dict:
             "UBSAN_OPTIONS": f"log_path={report_dir}/ubsan:halt_on_error=1:print_stacktrace=1"}
 
 
+def tsan_env(report_dir: str) -> dict:
+    """Environment for a ``*-tsan`` binary: one report file per process, any race fails it."""
+    return {"TSAN_OPTIONS": f"log_path={report_dir}/tsan:halt_on_error=1:exitcode=66:second_deadlock_stack=1"}
+
+
 def path_of(name: str) -> Path:
     return TARGETS[name][0]
 
 
 def _build_one(name: str, force: bool) -> tuple[str, str | None]:
     out, cmd = TARGETS[name]
-    srcs = [Path(c) for c in cmd if c.endswith((".cpp", ".hip"))] + DEPS.get(name.replace("-asan", ""), [])
+    srcs = [Path(c) for c in cmd if c.endswith((".cpp", ".hip"))] + \
+        DEPS.get(name.replace("-asan", "").replace("-tsan", ""), [])
     if not force and out.exists() and all(out.stat().st_mtime >= s.stat().st_mtime for s in srcs):
         return name, None
     if shutil.which(cmd[0]) is None and not Path(cmd[0]).exists():

@@ -466,6 +466,34 @@ extern "C" int thsmi_sample_json(char* buf, int cap) {
   return emit(s, buf, cap);
 }
 
+// The host half of a sample, without amdsmi: CPU utilisation / memory and every process that
+// has GPU memory (KFD sysfs + DRM fdinfo), attributed to owner and task -- under the same lock
+// as the full sample.  Works on a node whose GPUs amdsmi cannot open (and is what the TSan stress
+// test drives from several threads on a CPU-only host).
+extern "C" int thsmi_host_sample_json(char* buf, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const uint64_t ts = now_ns();
+  auto kfd = kfd_processes();
+  auto drm = drm_processes();
+  std::set<long> pids;
+  for (const auto& g : kfd)
+    for (long p : g.second) pids.insert(p);
+  for (const auto& d : drm)
+    for (const auto& p : d.second) pids.insert(p.first);
+  std::string s = "{\"ts_ns\":" + std::to_string(ts) + ",\"cpu\":" + cpu_json() + ",\"processes\":[";
+  bool first = true;
+  for (long p : pids) {
+    if (ignored_pid(p)) continue;
+    ProcInfo pi = resolve_pid(p);
+    if (pi.uid < 0 && pi.cmd.empty()) continue;
+    s += std::string(first ? "" : ",") + "{\"pid\":" + std::to_string(p) + ",\"command\":\"" + esc(pi.cmd) +
+         "\",\"owner\":\"" + esc(pi.owner) + "\"}";
+    first = false;
+  }
+  s += "]}";
+  return emit(s, buf, cap);
+}
+
 // Replace the ignore list (pids of the monitor's own helper processes); returns its size.
 extern "C" int thsmi_set_ignored_pids(const long* pids, int n) {
   std::lock_guard<std::mutex> lk(g_mu);

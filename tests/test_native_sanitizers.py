@@ -1,7 +1,9 @@
-"""AddressSanitizer + UndefinedBehaviorSanitizer runs of the native host tools (SURVEY §5 race /
-memory-error detection): the th-run supervisor's whole spawn / ls / status / wait / signal cycle,
-including its forked monitor process, and th-smi's start-up path, with every sanitizer report
-written to a file and asserted absent."""
+"""Sanitizer runs of the native host tools (SURVEY §5 race / memory-error detection):
+AddressSanitizer + UBSan and ThreadSanitizer builds of the th-run supervisor's whole spawn / ls /
+status / wait / signal cycle (including its forked monitor process), of th-smi's start-up path,
+and of libthsmi driven from four threads at once (``native/thsmi_stress.cpp``), with every
+sanitizer report written to a file and asserted absent.  The GPU-side TSan runs (full amdsmi
+sample, the th-counters reader) are in tests/gpu/test_native_gpu.py."""
 import os
 import shutil
 import subprocess
@@ -9,15 +11,15 @@ import time
 
 import pytest
 
-from tensorhive_fixed_amd.native.build import _build_one, path_of, sanitizer_env
+from tensorhive_fixed_amd.native.build import _build_one, path_of, sanitizer_env, tsan_env
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++ with libasan")
 
 
 def _build(name):
     _, err = _build_one(name, False)
-    if err and "libasan" in err:
-        pytest.skip("libasan not available")
+    if err and ("libasan" in err or "libtsan" in err):
+        pytest.skip("sanitizer runtime not available")
     assert err is None, err
     return str(path_of(name))
 
@@ -26,11 +28,13 @@ def _reports(d):
     return {p: open(os.path.join(d, p)).read()[-2000:] for p in os.listdir(d)}
 
 
-def test_th_run_under_asan_ubsan(tmp_path):
-    th = _build("th-run-asan")
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_th_run_under_sanitizers(tmp_path, kind):
+    th = _build(f"th-run-{kind}")
     rep = tmp_path / "reports"
     rep.mkdir()
-    env = {**os.environ, "TH_RUN_STATE_DIR": str(tmp_path / "state"), **sanitizer_env(str(rep))}
+    san = sanitizer_env(str(rep)) if kind == "asan" else tsan_env(str(rep))
+    env = {**os.environ, "TH_RUN_STATE_DIR": str(tmp_path / "state"), **san}
 
     def run(*a, timeout=30):
         return subprocess.run([th, *a], capture_output=True, text=True, env=env, timeout=timeout)
@@ -65,4 +69,18 @@ def test_th_smi_startup_under_asan(tmp_path):
                        env={**os.environ, **sanitizer_env(str(rep))})
     # no GPU here: amdsmi init fails cleanly; on a GPU node it prints one JSON sample
     assert r.returncode in (0, 1) and (r.returncode == 1 or r.stdout.startswith("{"))
+    assert _reports(rep) == {}
+
+
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_libthsmi_from_four_threads(tmp_path, kind):
+    """Two threads sampling the host half (CPU + KFD/DRM process scan), one the full sample and
+    topology (when amdsmi is up), one rewriting the ignore list -- no race, no memory error."""
+    exe = _build(f"thsmi-stress-{kind}")
+    rep = tmp_path / "reports"
+    rep.mkdir()
+    san = sanitizer_env(str(rep)) if kind == "asan" else tsan_env(str(rep))
+    r = subprocess.run([exe, "--iters", "120"], capture_output=True, text=True, timeout=300, env={**os.environ, **san})
+    assert r.returncode == 0, (r.stdout, r.stderr[-2000:], _reports(rep))
+    assert '"bad":0' in r.stdout
     assert _reports(rep) == {}
