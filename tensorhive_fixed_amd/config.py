@@ -235,6 +235,8 @@ class AmdMonitorConfig:
     stub_gpus: int
     counters_enabled: bool = False
     counters_period_ms: int = 1000
+    # tasks count their own HBM bytes (libthhbm via ROCP_TOOL_LIBRARIES, core/hbm.py)
+    task_hbm_counters: bool = True
 
 
 @dataclass
@@ -408,6 +410,7 @@ def load_config(directory: Path | str | None = None) -> Config:
             stub_gpus=main.int("amd_monitor", "stub_gpus", 8),
             counters_enabled=main.bool("amd_monitor", "counters_enabled", False),
             counters_period_ms=main.int("amd_monitor", "counters_period_ms", 1000),
+            task_hbm_counters=main.bool("amd_monitor", "task_hbm_counters", True),
         ),
         launcher=LauncherConfig(
             supervisor=main.str("launcher", "supervisor", "th-run"),

@@ -94,9 +94,23 @@ def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | No
     return f"if command -v {th} >/dev/null 2>&1 || [ -x {th} ]; then {primary}; else {fallback}; fi"
 
 
+def spawn_env(hostname: str) -> dict[str, str]:
+    """Environment th-run gives every task on ``hostname`` besides ``TENSORHIVE_TASK_ID``: on the
+    daemon's own node, the in-task HBM counter tool (``[amd_monitor] task_hbm_counters``,
+    ``core/hbm.py``), whose per-process files only the local monitor reads."""
+    cfg = get_config()
+    spec = cfg.ssh.available_nodes.get(hostname, {})
+    if spec.get("transport") == "local" and getattr(cfg.amd_monitor, "task_hbm_counters", False):
+        from .hbm import task_env
+
+        return task_env()
+    return {}
+
+
 def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra_env: dict | None = None,
           max_restarts: int = 0) -> int:
-    r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), extra_env,
+    env = {**spawn_env(hostname), **(extra_env or {})}
+    r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), env,
                                                  max_restarts))
     if r.exception is not None:
         raise SpawnError(f"connection failed: {r.exception}")

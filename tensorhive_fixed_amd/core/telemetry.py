@@ -74,7 +74,8 @@ class AmdSmiBackend(TelemetryBackend):
     name = "amdsmi"
 
     def __init__(self, probe: bool = False, probe_period: float = 1.0, counters: bool = False,
-                 counters_period_ms: int = 1000):
+                 counters_period_ms: int = 1000, task_hbm: bool = True):
+        self.task_hbm = task_hbm
         if not NATIVE_LIB.exists():
             from ..native.build import build_all
 
@@ -143,6 +144,13 @@ class AmdSmiBackend(TelemetryBackend):
                 m = by_kfd.get(g.get("kfd_id"))
                 if m:
                     extra.setdefault(g["index"], {}).update(m)
+        if self.task_hbm:  # HBM bytes counted inside the tasks themselves (core/hbm.py)
+            from . import hbm
+
+            counted = hbm.metrics_for(doc.get("gpus", []), hbm.read_rates())
+            for g in doc.get("gpus", []):
+                extra.setdefault(g["index"], {}).update(
+                    counted.get(g["index"], {"hbm_bw_source": _metric("umc_activity", "")}))
         return entry_from_thsmi(host, doc, extra or None)
 
     def topology(self, host: str) -> dict | None:
@@ -438,7 +446,7 @@ class StubBackend(TelemetryBackend):
 
 def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, probe: bool = False,
                  probe_period: float = 1.0, stream_ms: int | None = None, counters: bool = False,
-                 counters_period_ms: int = 1000) -> TelemetryBackend:
+                 counters_period_ms: int = 1000, task_hbm: bool = True) -> TelemetryBackend:
     """Pick a backend for ``host``: ``auto`` = amdsmi for the local node when /dev/kfd exists,
     remote th-smi for ssh nodes, stub otherwise."""
     spec_local = transports is None or getattr(transports.transports.get(host), "__class__", None).__name__ == "LocalTransport"
@@ -446,7 +454,7 @@ def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, prob
         return StubBackend(stub_gpus)
     if kind == "amdsmi" or (kind == "auto" and spec_local and os.path.exists("/dev/kfd")):
         return AmdSmiBackend(probe=probe, probe_period=probe_period, counters=counters,
-                             counters_period_ms=counters_period_ms)
+                             counters_period_ms=counters_period_ms, task_hbm=task_hbm)
     if kind == "remote" or (kind == "auto" and not spec_local):
         return RemoteBackend(transports, stream_ms=stream_ms)
     return StubBackend(stub_gpus)

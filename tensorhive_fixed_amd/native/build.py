@@ -7,6 +7,7 @@ Targets (all into ``native/bin`` / ``native/lib``; git-ignored, shipped with the
   * ``bin/rccl-bench``    -- RCCL/xGMI collective + direct P2P all-reduce bench      [hipcc + librccl]
   * ``bin/th-counters``   -- device-wide HW counter sampler (rocprofiler-sdk)       [g++ + rocprofiler-sdk]
   * ``bin/th-probe``      -- per-node probe agent: the gfx950 probe kernel on every GPU [hipcc]
+  * ``lib/libthhbm.so``   -- in-task HBM byte counters (rocprofiler-sdk tool library)  [g++ + rocprofiler-sdk]
 The gfx950 training kernels (and the same probe kernel, for in-process use) are built by
 :mod:`..ops.build` into ``libthk.so``.
 """
@@ -38,6 +39,9 @@ TARGETS = {
     "th-counters": (BIN / "th-counters", [CXX, "-O2", "-std=c++17", f"-I{ROCM}/include",
                                           str(HERE / "th_counters.cpp"), f"-L{ROCM}/lib", "-lrocprofiler-sdk",
                                           "-lhsa-runtime64", f"-Wl,-rpath,{ROCM}/lib"]),
+    "libthhbm": (LIB / "libthhbm.so", [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", f"-I{ROCM}/include",
+                                       str(HERE / "th_hbm_tool.cpp"), f"-L{ROCM}/lib", "-lrocprofiler-sdk",
+                                       f"-Wl,-rpath,{ROCM}/lib"]),
     "th-probe": (BIN / "th-probe", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", f"-I{KSRC}",
                                     str(HERE / "th_probe.hip")]),
     "rccl-bench": (BIN / "rccl-bench", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}",

@@ -1,7 +1,16 @@
-"""HBM bandwidth telemetry against a timed device stream (round-2 verdict, missing item 4):
-libthsmi's ``hbm_bw`` (calibrated ``mem_activity_acc`` rate) must be within +-15 % of the GB/s a
-tenant process measures for its own copy loop."""
+"""HBM bandwidth on the dashboard from hardware counters (round-2 verdict item 3).
+
+A task started the way th-run starts it (``ROCP_TOOL_LIBRARIES`` = the in-task counter tool,
+core/hbm.py) is sampled by the local monitor; its ``hbm_bw`` (``hbm_bw_source == counters``)
+must be within +-15 % of
+  (a) the bytes a copy stream moves by construction, per second, and
+  (b) the GEMM + SwiGLU mix of the training step: rocprofv3 dispatch-mode PMC bytes per
+      iteration of the same counters x the iterations per second of the sampled run.
+Without the tool, the activity-based estimate is reported and labelled ``umc_activity``."""
+import csv
 import json
+import os
+import shutil
 import subprocess
 import sys
 import time
@@ -12,30 +21,91 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[2]
+PMC = ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum"]
 
 
-def test_hbm_bw_tracks_a_timed_copy_stream():
+def _tool():
+    from tensorhive_fixed_amd.core import hbm
+    from tensorhive_fixed_amd.native.build import _build_one
+
+    _build_one("libthhbm", False)
+    p = hbm.tool_path()
+    assert p, "libthhbm.so not built"
+    return p
+
+
+def _sample_during(script_args, env, seconds=2.5, settle=2.0):
     from tensorhive_fixed_amd.core.telemetry import AmdSmiBackend
 
-    be = AmdSmiBackend()
+    be = AmdSmiBackend(task_hbm=True)
     try:
-        p = subprocess.Popen([sys.executable, str(ROOT / "scripts" / "hbm_stream.py"), "5", "copy"],
-                             stdout=subprocess.PIPE, text=True, cwd=ROOT)
-        time.sleep(2.0)  # past allocation + warm-up
-        vals = []
-        t_end = time.time() + 2.5
+        p = subprocess.Popen([sys.executable, *script_args], stdout=subprocess.PIPE, text=True, cwd=ROOT,
+                             env={**os.environ, **env})
+        time.sleep(settle)
+        vals, sources = [], set()
+        t_end = time.time() + seconds
         while time.time() < t_end:
-            doc = be.sample("localhost")
-            g = sorted(doc["GPU"].values(), key=lambda g: g["index"])[0]
-            v = g["metrics"]["hbm_bw"]["value"]
-            if v is not None:
-                vals.append(v)
+            g = sorted(be.sample("localhost")["GPU"].values(), key=lambda g: g["index"])[0]["metrics"]
+            sources.add(g["hbm_bw_source"]["value"])
+            if g["hbm_bw_source"]["value"] == "counters":
+                vals.append(g["hbm_bw"]["value"])
             time.sleep(0.25)
-        out, _ = p.communicate(timeout=60)
-        stream = json.loads(out.strip().splitlines()[-1])
+        out, _ = p.communicate(timeout=120)
+        assert p.returncode == 0
+        return vals, sources, json.loads(out.strip().splitlines()[-1])
     finally:
         be.close()
-    assert vals, "hbm_bw never reported"
+
+
+def test_counted_hbm_bw_tracks_a_copy_stream():
+    env = {"ROCP_TOOL_LIBRARIES": _tool(), "TH_HBM_PERIOD_MS": "500"}
+    vals, sources, stream = _sample_during([str(ROOT / "scripts" / "hbm_stream.py"), "6", "copy"], env)
+    assert vals, f"no counter-based sample (sources {sources})"
     measured = sorted(vals)[len(vals) // 2]
-    print(f"hbm_bw telemetry median {measured:.0f} GB/s vs timed stream {stream['GBps']:.0f} GB/s")
+    print(f"counted hbm_bw median {measured:.0f} GB/s vs copy stream {stream['GBps']:.0f} GB/s")
     assert abs(measured - stream["GBps"]) <= 0.15 * stream["GBps"], (vals, stream)
+
+
+def _pmc_bytes_per_iter(tmp_path) -> float:
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        pytest.skip("rocprofv3 not available")
+    out = tmp_path / "pmc"
+    r = subprocess.run([rp, "--pmc", *PMC, "-d", str(out), "-o", "run", "--output-format", "csv", "--",
+                        sys.executable, str(ROOT / "scripts" / "hbm_mix.py"), "1"],
+                       capture_output=True, text=True, timeout=240, cwd="/tmp", env={**os.environ, "TMPDIR": "/tmp"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    iters = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["iters"]
+    tot = dict.fromkeys(PMC, 0.0)
+    for f in out.rglob("*counter_collection.csv"):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] in tot:
+                    tot[row["Counter_Name"]] += float(row["Counter_Value"])
+    rd = 128 * tot["TCC_EA0_RDREQ_128B_sum"] + 64 * (tot["TCC_EA0_RDREQ_sum"] - tot["TCC_EA0_RDREQ_128B_sum"])
+    wr = 64 * tot["TCC_EA0_WRREQ_64B_sum"] + 32 * (tot["TCC_EA0_WRREQ_sum"] - tot["TCC_EA0_WRREQ_64B_sum"])
+    assert iters > 0 and rd > 0
+    return (rd + wr) / iters
+
+
+def test_counted_hbm_bw_matches_dispatch_pmc_on_the_gemm_swiglu_mix(tmp_path):
+    per_iter = _pmc_bytes_per_iter(tmp_path)  # bytes per iteration, rocprofv3 dispatch mode
+    env = {"ROCP_TOOL_LIBRARIES": _tool(), "TH_HBM_PERIOD_MS": "500"}
+    vals, sources, run = _sample_during([str(ROOT / "scripts" / "hbm_mix.py"), "6"], env)
+    assert vals, f"no counter-based sample (sources {sources})"
+    expected = per_iter * run["iters"] / run["seconds"] / 1e9
+    measured = sorted(vals)[len(vals) // 2]
+    print(f"counted hbm_bw median {measured:.0f} GB/s vs dispatch PMC {per_iter / 1e9:.3f} GB/iter x "
+          f"{run['iters'] / run['seconds']:.1f} iter/s = {expected:.0f} GB/s")
+    assert abs(measured - expected) <= 0.15 * expected, (vals, expected)
+
+
+def test_without_the_tool_the_estimate_is_labelled():
+    from tensorhive_fixed_amd.core.telemetry import AmdSmiBackend
+
+    be = AmdSmiBackend(task_hbm=True)
+    try:
+        g = sorted(be.sample("localhost")["GPU"].values(), key=lambda g: g["index"])[0]["metrics"]
+    finally:
+        be.close()
+    assert g["hbm_bw_source"]["value"] == "umc_activity"
