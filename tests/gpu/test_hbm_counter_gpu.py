@@ -34,14 +34,15 @@ def _tool():
     return p
 
 
-def _sample_during(script_args, env, seconds=2.5, settle=2.0):
+def _sample_during(script_args, env, seconds=2.5, settle=1.2):
     from tensorhive_fixed_amd.core.telemetry import AmdSmiBackend
 
     be = AmdSmiBackend(task_hbm=True)
     try:
         p = subprocess.Popen([sys.executable, *script_args], stdout=subprocess.PIPE, text=True, cwd=ROOT,
                              env={**os.environ, **env})
-        time.sleep(settle)
+        assert json.loads(p.stdout.readline()) == {"ready": True}  # the load runs from here on
+        time.sleep(settle)  # > two tool periods: a whole window of the load has been published
         vals, sources = [], set()
         t_end = time.time() + seconds
         while time.time() < t_end:
