@@ -283,6 +283,179 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt16_kernel(const ushort* __rest
     }
 }
 
+// Variants of the 16x16x32 kernel for the round-3 hipBLASLt-parity probe (profiles/r03_gemm):
+//   * AHEAD / NS: DMA depth.  AHEAD 3 with a 5-stage ring (the whole 160 KB LDS) gives every
+//     k-tile's LDS-DMA three k-tiles (six slots) to land instead of two;
+//   * PRIO: s_setprio 1 around each wave's MFMA block (the guide's T5 static form);
+//   * LDSEPI: the output tile leaves through LDS as whole rows -- each lane stores 16 B (8 columns)
+//     per instruction instead of 2-B scalars at a 64-row stride (guide T21 / "O staged through
+//     LDS"): the f32 accumulators of one group's 64-row half are written to a padded [64][260] f32
+//     image (row stride 1040 B: the 4 row groups of a wave land 16 banks apart), then all 512
+//     threads read 8 consecutive columns each and store them (C += in f32 when BETA), 4 rounds.
+template <bool BETA, int AHEAD, int NS, bool PRIO, bool LDSEPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt16v_kernel(const ushort* __restrict__ A, long lda,
+                                                            const ushort* __restrict__ B, long ldb,
+                                                            ushort* __restrict__ C, long ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[NS * STAGEB];
+  char LDS_AS* smem = (char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = L / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = L % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3, w4 = w & 3;
+  const bool g1 = w >= 4;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int nt = K / TK;
+
+  const int i16 = lane & 15, kg = lane >> 4;
+  const int chk = (kg ^ ((i16 >> 2) & 3)) * 16;
+  int a_row[8], b_row[4];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) a_row[mb] = (wm * 128 + 16 * mb + i16) * ROWB + chk;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) b_row[nb] = (wn * 64 + 16 * nb + i16) * ROWB + chk;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4(0.f);
+
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  const unsigned la = lane_off_nt(lda, lane), lb = lane_off_nt(ldb, lane);
+#pragma unroll
+  for (int j = 0; j < AHEAD; ++j) {
+    if (j < nt) {
+      if (!g1) stage_nt(A, la, lda, m0, (long)j * TK, lds0 + j * STAGEB, w4);
+      else stage_nt(B, lb, ldb, n0, (long)j * TK, lds0 + j * STAGEB + OPB, w4);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  if (g1) asm volatile("s_barrier" ::: "memory");
+
+  int cur = 0, nxt = AHEAD % NS;  // ring slots of k-tile t and of k-tile t + AHEAD
+  bf16x8 af[8], bf[4];
+  for (int t = 0; t < nt; ++t) {
+    const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
+    if (t + AHEAD < nt) {
+      const unsigned st = lds0 + nxt * STAGEB;
+      if (!g1) stage_nt(A, la, lda, m0, (long)(t + AHEAD) * TK, st, w4);
+      else stage_nt(B, lb, ldb, n0, (long)(t + AHEAD) * TK, st + OPB, w4);
+    }
+    const char LDS_AS* sa = smem + cur * STAGEB;
+    const char LDS_AS* sb = sa + OPB;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) af[mb] = lds_b128(sa + a_row[mb]);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) bf[nb] = lds_b128(sb + b_row[nb]);
+    auto wait_barrier = [&]() {
+      if (AHEAD >= 3 && younger >= 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else if (younger >= 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    if (g1) wait_barrier();
+    else asm volatile("s_barrier" ::: "memory");
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma16(af[mb], bf[nb], acc[mb][nb]);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!g1) wait_barrier();
+    else asm volatile("s_barrier" ::: "memory");
+    cur = cur + 1 == NS ? 0 : cur + 1;
+    nxt = nxt + 1 == NS ? 0 : nxt + 1;
+  }
+  if (!g1) asm volatile("s_barrier" ::: "memory");
+
+  if (!LDSEPI) {
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const long n = n0 + wn * 64 + 16 * nb + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long m = m0 + wm * 128 + 16 * mb + 4 * kg + r;
+          float v = acc[mb][nb][r];
+          if (BETA) v += bf2f(C[m * ldc + n]);
+          C[m * ldc + n] = f2bf(v);
+        }
+      }
+    return;
+  }
+  // ---- epilogue through LDS: 4 rounds of 64 output rows (group g, half h of its 128 rows)
+  constexpr int EROW = 260;  // f32 per padded image row
+  float LDS_AS* img = (float LDS_AS*)smem;
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done with the ring
+#pragma unroll
+  for (int round = 0; round < 4; ++round) {
+    const int g = round >> 1, h = round & 1;
+    if ((int)g1 == g) {
+#pragma unroll
+      for (int mbh = 0; mbh < 4; ++mbh)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * mbh + 4 * kg + r, col = wn * 64 + 16 * nb + i16;
+            img[row * EROW + col] = acc[4 * h + mbh][nb][r];
+          }
+    }
+    __syncthreads();
+    // 64 rows x 32 chunks of 8 columns = 2048 chunks over 512 threads
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = tid + q * NTHR, row = c >> 5, col8 = (c & 31) * 8;
+      const float LDS_AS* src = img + row * EROW + col8;
+      const float4v lo = *reinterpret_cast<const float4v LDS_AS*>(src);
+      const float4v hi = *reinterpret_cast<const float4v LDS_AS*>(src + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      ushort* dst = C + (m0 + g * 128 + h * 64 + row) * ldc + n0 + col8;
+      if (BETA) {
+        const ushort8 old = *reinterpret_cast<const ushort8*>(dst);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += bf2f(old[j]);
+      }
+      ushort8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+      *reinterpret_cast<ushort8*>(dst) = o;
+    }
+    __syncthreads();
+  }
+}
+
+template <bool BETA>
+static void launch_nt16v(int variant, unsigned grid, hipStream_t s, const ushort* A, long lda, const ushort* B,
+                         long ldb, ushort* C, long ldc, int M, int N, int K) {
+  // variant bits: 1 = deep ring (AHEAD 3, 5 stages), 2 = setprio, 4 = LDS epilogue
+  switch (variant & 7) {
+#define TH_NT16V(V, AH, NSS, PR, LE)                                                                            \
+  case V:                                                                                                     \
+    gemm_nt16v_kernel<BETA, AH, NSS, PR, LE><<<grid, NTHR, 0, s>>>(A, lda, B, ldb, C, ldc, M, N, K);          \
+    break;
+    TH_NT16V(0, 2, 4, false, false)
+    TH_NT16V(1, 3, 5, false, false)
+    TH_NT16V(2, 2, 4, true, false)
+    TH_NT16V(3, 3, 5, true, false)
+    TH_NT16V(4, 2, 4, false, true)
+    TH_NT16V(5, 3, 5, false, true)
+    TH_NT16V(6, 2, 4, true, true)
+    TH_NT16V(7, 3, 5, true, true)
+#undef TH_NT16V
+  }
+}
+
 // C[M][N] (+)= A[M][K] B[N][K]^T (row strides lda, ldb, ldc in elements).  -1: shape not tiled.
 extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                           int beta, int flags, hipStream_t s) {
@@ -292,6 +465,14 @@ extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   // the lane offset and the per-instruction scalar bases stay within 32-bit byte offsets per row block
   if ((long)16 * lda * 2 >= (1L << 31) || (long)16 * ldb * 2 >= (1L << 31)) return -1;
   const unsigned grid = (unsigned)((long)(M / TM) * (N / TN));
+  if (flags & 14) {  // round-3 variants of the 16x16x32 kernel: flags bits 1-3 = variant bits 0-2
+    const int v = (flags >> 1) & 7;
+    if (beta)
+      launch_nt16v<true>(v, grid, s, (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
+    else
+      launch_nt16v<false>(v, grid, s, (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
+    TH_CHECK_LAUNCH();
+  }
   if (flags & 1) {  // 16x16x32 MFMA variant
     if (beta)
       gemm_nt16_kernel<true><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);

@@ -15,8 +15,12 @@ def supported(m: int, n: int, k: int) -> bool:
 
 
 def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-             mfma16: bool = False) -> torch.Tensor:
-    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation)."""
+             mfma16: bool = False, variant: int = 0) -> torch.Tensor:
+    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation).
+
+    ``variant`` (1-7, 16x16x32 kernel only) selects the round-3 probe variants of
+    ``csrc/gemm_nt.hip``: bit 0 = 3-deep DMA in a 5-stage ring, bit 1 = s_setprio around the MFMA
+    blocks, bit 2 = output through LDS as 16-B row stores."""
     M, K = a.shape
     N, K2 = b.shape
     if K2 != K or tuple(out.shape) != (M, N):
@@ -30,5 +34,5 @@ def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
             torch.mm(a, b.t(), out=out)
         return out
     _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), int(mfma16), _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), int(mfma16) | ((int(variant) & 7) << 1), _lib.stream_ptr(a.device))
     return out
