@@ -13,7 +13,7 @@ for d in sys.argv[1:]:
             short = name.replace("(anonymous namespace)::", "").split("(")[0][:60]
             acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in sorted(acc.items()):
-    if not any(x in k for x in ("fa_", "flash", "Cijk", "rmsnorm", "swiglu", "gemm_tn")):
+    if not any(x in k for x in ("fa_", "flash", "Cijk", "rmsnorm", "swiglu", "gemm_tn", "gemm_nt")):
         continue
     print(k)
     for c, v in sorted(cs.items()):

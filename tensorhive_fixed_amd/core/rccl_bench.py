@@ -83,14 +83,15 @@ def run_single(gpus: int = 0, min_bytes: int = 8 << 20, max_bytes: int = 1 << 30
 
 def run_per_rank(gpus: int, min_bytes: int = 8 << 20, max_bytes: int = 1 << 30, iters: int = 20, op: str = "all",
                  env: dict | None = None, timeout: float = 600) -> dict:
-    """``torchrun --no-python --nproc-per-node GPUS rccl-bench --per-rank ...`` (one rank per GPU)."""
+    """``TH_RCCL_PER_RANK=1 torchrun --no-python --nproc-per-node GPUS rccl-bench`` (one rank per
+    GPU; the options travel in the environment, torchrun's parser would claim ``--min``/``--max``)."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python", _binary(), "--per-rank",
-           "--min", str(min_bytes), "--max", str(max_bytes), "--iters", str(iters), "--op", op]
-    e = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0", **(env or {})}
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "--no-python", _binary()]
+    e = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0", "TH_RCCL_PER_RANK": "1", "TH_RCCL_MIN": str(min_bytes),
+         "TH_RCCL_MAX": str(max_bytes), "TH_RCCL_ITERS": str(iters), "TH_RCCL_OP": op, **(env or {})}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
     if r.returncode != 0:
         raise RuntimeError(f"rccl-bench --per-rank failed ({r.returncode}): {r.stderr[-2000:]}")

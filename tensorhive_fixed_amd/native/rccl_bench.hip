@@ -4,9 +4,11 @@
 //   * single process (default): one process drives every visible GPU (ncclCommInitAll), runs
 //     without a launcher;
 //   * --per-rank: one process per GPU, as the training job runs -- started by torchrun
-//     (`torchrun --no-python --nproc-per-node N rccl-bench --per-rank`), RANK / WORLD_SIZE /
-//     LOCAL_RANK from the environment, ncclCommInitRank with a unique id that rank 0 publishes in
-//     a file (no MPI); every rank times its own loop and the MAX over ranks is reported.
+//     (`TH_RCCL_PER_RANK=1 torchrun --no-python --nproc-per-node N rccl-bench`), RANK / WORLD_SIZE
+//     / LOCAL_RANK from the environment, ncclCommInitRank with a unique id that rank 0 publishes
+//     in a file (no MPI); every rank times its own loop and the MAX over ranks is reported.  Under
+//     torchrun the options travel as TH_RCCL_MIN / _MAX / _ITERS / _OP (torchrun's own parser
+//     would take --min / --max for abbreviations of its options).
 //   rccl-bench [--per-rank] [--gpus N] [--min BYTES] [--max BYTES] [--iters K]
 //              [--op allreduce|reducescatter|allgather|all] [--direct] | --check-virtual-peers P [--min BYTES]
 // Output (JSON lines; schema pinned by core/rccl_bench.py and tests/test_rccl_bench.py): one
@@ -316,6 +318,13 @@ int main(int argc, char** argv) {
                       "       rccl-bench --check-virtual-peers P [--min B]\n");
       return 2;
     }
+  }
+  if (getenv("TH_RCCL_PER_RANK") && !strcmp(getenv("TH_RCCL_PER_RANK"), "1")) {
+    rank_mode = true;
+    if (getenv("TH_RCCL_MIN")) mn = atol(getenv("TH_RCCL_MIN"));
+    if (getenv("TH_RCCL_MAX")) mx = atol(getenv("TH_RCCL_MAX"));
+    if (getenv("TH_RCCL_ITERS")) iters = atoi(getenv("TH_RCCL_ITERS"));
+    if (getenv("TH_RCCL_OP")) op = getenv("TH_RCCL_OP");
   }
   if (mn < 16 || mx < mn || iters < 1) return 2;
   if (vpeers > 0) {
