@@ -86,6 +86,16 @@ def tsan_env(report_dir: str) -> dict:
     return {"TSAN_OPTIONS": f"log_path={report_dir}/tsan:halt_on_error=1:exitcode=66:second_deadlock_stack=1"}
 
 
+def tsan_argv(exe: str, *args: str) -> list[str]:
+    """Command line for a ``*-tsan`` binary: under ``setarch -R`` (no address randomisation) when
+    available -- ThreadSanitizer aborts with "unexpected memory mapping" on kernels whose mmap
+    randomisation places libraries outside its shadow layout (seen on the MI355X boxes)."""
+    import platform
+
+    sa = shutil.which("setarch")
+    return ([sa, platform.machine(), "-R"] if sa else []) + [exe, *args]
+
+
 def path_of(name: str) -> Path:
     return TARGETS[name][0]
 

@@ -199,7 +199,7 @@ def test_rccl_bench_both_modes_on_one_gpu():
 def test_native_tools_under_tsan_on_the_gpu(tmp_path):
     """ThreadSanitizer on the GPU-side paths: libthsmi's full amdsmi sample from four threads and
     the th-counters reader (its sampling loop beside rocprofiler-sdk's threads)."""
-    from tensorhive_fixed_amd.native.build import _build_one, path_of, tsan_env
+    from tensorhive_fixed_amd.native.build import _build_one, path_of, tsan_argv, tsan_env
 
     for name in ("thsmi-stress-tsan", "th-counters-tsan"):
         _, err = _build_one(name, False)
@@ -207,10 +207,10 @@ def test_native_tools_under_tsan_on_the_gpu(tmp_path):
     rep = tmp_path / "reports"
     rep.mkdir()
     env = {**os.environ, **tsan_env(str(rep))}
-    r = subprocess.run([str(path_of("thsmi-stress-tsan")), "--iters", "40"], capture_output=True, text=True,
+    r = subprocess.run(tsan_argv(str(path_of("thsmi-stress-tsan")), "--iters", "40"), capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 0 and '"bad":0' in r.stdout and '"gpus":-1' not in r.stdout, (r.stdout, r.stderr[-2000:])
-    r = subprocess.run([str(path_of("th-counters-tsan")), "--count", "2", "--window", "100", "--period", "200"],
+    r = subprocess.run(tsan_argv(str(path_of("th-counters-tsan")), "--count", "2", "--window", "100", "--period", "200"),
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     reports = {p.name: p.read_text()[-3000:] for p in rep.iterdir()}

@@ -11,7 +11,7 @@ import time
 
 import pytest
 
-from tensorhive_fixed_amd.native.build import _build_one, path_of, sanitizer_env, tsan_env
+from tensorhive_fixed_amd.native.build import _build_one, path_of, sanitizer_env, tsan_argv, tsan_env
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++ with libasan")
 
@@ -37,7 +37,8 @@ def test_th_run_under_sanitizers(tmp_path, kind):
     env = {**os.environ, "TH_RUN_STATE_DIR": str(tmp_path / "state"), **san}
 
     def run(*a, timeout=30):
-        return subprocess.run([th, *a], capture_output=True, text=True, env=env, timeout=timeout)
+        argv = tsan_argv(th, *a) if kind == "tsan" else [th, *a]
+        return subprocess.run(argv, capture_output=True, text=True, env=env, timeout=timeout)
 
     r = run("spawn", "--name", "tensorhive_task_a", "--log", str(tmp_path / "a.log"), "--env", "X=1", "--",
             "bash", "-c", "echo $X; exit 3")
@@ -80,7 +81,8 @@ def test_libthsmi_from_four_threads(tmp_path, kind):
     rep = tmp_path / "reports"
     rep.mkdir()
     san = sanitizer_env(str(rep)) if kind == "asan" else tsan_env(str(rep))
-    r = subprocess.run([exe, "--iters", "120"], capture_output=True, text=True, timeout=300, env={**os.environ, **san})
+    argv = tsan_argv(exe, "--iters", "120") if kind == "tsan" else [exe, "--iters", "120"]
+    r = subprocess.run(argv, capture_output=True, text=True, timeout=300, env={**os.environ, **san})
     assert r.returncode == 0, (r.stdout, r.stderr[-2000:], _reports(rep))
     assert '"bad":0' in r.stdout
     assert _reports(rep) == {}
