@@ -34,5 +34,5 @@ def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
             torch.mm(a, b.t(), out=out)
         return out
     _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), int(mfma16) | ((int(variant) & 7) << 1), _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), int(mfma16) | ((int(variant) & 7) << 1) , _lib.stream_ptr(a.device))
     return out
