@@ -83,7 +83,9 @@ def sanitizer_env(report_dir: str) -> dict:
 
 def tsan_env(report_dir: str) -> dict:
     """Environment for a ``*-tsan`` binary: one report file per process, any race fails it."""
-    return {"TSAN_OPTIONS": f"log_path={report_dir}/tsan:halt_on_error=1:exitcode=66:second_deadlock_stack=1"}
+    supp = HERE / "tsan.supp"  # vendor-library findings only, each one justified in the file
+    return {"TSAN_OPTIONS": f"log_path={report_dir}/tsan:halt_on_error=1:exitcode=66:second_deadlock_stack=1:"
+                            f"suppressions={supp}"}
 
 
 def tsan_argv(exe: str, *args: str) -> list[str]:
