@@ -1299,6 +1299,238 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
                   scale_log2, causal);
 }
 
+// ------------------------------------ paired dK | dV kernel, half width: two workgroups per CU
+// The same roles and MFMA work as kc_body (DMA mode), in workgroups of 4 waves over 64 keys: one
+// dK wave and one dV wave per 32-key slice, two slices.  The 8-wave kernel holds one workgroup per
+// CU, so its 8 waves pass the same two barriers per tile together and every phase boundary
+// (barrier, first LDS operands, MFMA -> exp) is exposed on all of them at once (39.8 % MFMA busy,
+// profiles/r02_flash).  With two independent workgroups per CU the waves of one SIMD belong to
+// different barrier domains, as in the dQ kernel (60.5 % busy).  LDS per workgroup: two Q|dO
+// tiles (DMA double buffer) + the P exchange of the two pairs, as bf16 (the value the dV MFMA
+// consumes): 2 x 33 KB + 8 KB = 73 KB, two workgroups = 146 KB of the 160 KB.
+constexpr int KH_BK = 64, KH_LDS = 2 * KC_TILE + 2 * 4096;
+
+template <bool DK>
+__device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
+                                        const float* __restrict__ LSE, const float* __restrict__ Dl,
+                                        const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
+                                        char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
+                                        long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  // role-local ids: waves 0-1 are the dK role, 2-3 the dV role of the same 64 keys
+  const int tid = threadIdx.x & 127, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  // P exchange of pair w: [half][s0 | s1][lane] bf16x8, 4 KB
+  bf16x8* pbuf = reinterpret_cast<bf16x8*>(smem + 2 * KC_TILE + w * 4096);
+  const int k0 = kblk0 + 32 * w;
+  const int key = k0 + c32;
+  const ushort* fb = DK ? Vb : Kb;
+  bf16x8 kf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    ushort8 u = key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0);
+    if (!DK) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
+    }
+    kf[s] = as_bf(u);
+  }
+  f32x16 acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
+
+  const int nqt = (S + C_BQ - 1) / C_BQ;
+  const int qt0 = causal ? kblk0 / C_BQ : 0;
+  const int per_head = nqt - qt0;
+  const int total = G * per_head;
+  // each role's 2 waves DMA its 16 KB image (Q for dK, dO for dV): 8 x 1 KB per wave
+  unsigned rc[8];
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto dma_tile = [&](int h_i, int t_i, int buf) {
+    const int hq = hk * G + h_i;
+    const int qq0 = (qt0 + t_i) * C_BQ;
+    const ushort* base = DK ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
+    const long ldx = DK ? ld : ldo;
+    const unsigned img = lds0 + buf * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 8192;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
+      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
+    }
+  };
+  float lr = 0.f, dr = 0.f;
+  int lq = 0;
+  auto load_ld = [&](int h_i, int t_i) {
+    if (DK && tid < C_BQ) {
+      const int hq = hk * G + h_i;
+      lq = (qt0 + t_i) * C_BQ + tid;
+      const long st = ((long)b * Hq + hq) * S;
+      const int qc = min(lq, S - 1);
+      lr = LSE[st + qc];
+      dr = Dl[st + qc];
+    }
+  };
+  auto write_ld = [&](int buf) {
+    if (DK && tid < C_BQ) {
+      float* l = reinterpret_cast<float*>(smem + buf * KC_TILE + 2 * C_BQ * 256);
+      l[tid] = lq < S ? -lr * LOG2E : -INFINITY;  // negated (initial accumulators); past S: P = 0
+      l[C_BQ + tid] = lq < S ? -dr : 0.f;
+    }
+  };
+  int pf_h = 0, pf_t = 0, lh = 0, lt = 0, cur_t = 0;
+  auto adv = [&](int& hh, int& tt) {
+    if (++tt == per_head) { tt = 0; ++hh; }
+  };
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // K/V fragment loads retired (a wait the compiler sees)
+#pragma unroll
+  for (int u = 0; u < 8; ++u) rc[u] = img_rc(wu * 8192 + u * 1024 + lane * 16);
+  if (total > 0) {
+    load_ld(0, 0);
+    write_ld(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    dma_tile(0, 0, 0);
+    adv(lh, lt);
+    if (total > 1) load_ld(lh, lt);
+  }
+  for (int it = 0; it < total; ++it) {
+    char* cur = smem + (it & 1) * KC_TILE;
+    wait_dma_barrier();  // tile it landed; every wave is past tile it-1 (its buffer is free)
+    if (it + 1 < total) {
+      write_ld((it + 1) & 1);
+      adv(pf_h, pf_t);
+      dma_tile(pf_h, pf_t, (it + 1) & 1);
+      adv(lh, lt);
+      if (it + 2 < total) load_ld(lh, lt);
+    }
+    const char* qs = cur;
+    const char* gs = cur + C_BQ * 256;
+    const float* ls = reinterpret_cast<const float*>(cur + 2 * C_BQ * 256);
+    const float* ds = ls + C_BQ;
+    const int qbase = (qt0 + cur_t) * C_BQ;
+    if (++cur_t == per_head) cur_t = 0;
+    // phase 1: dK role dP' = dO V^T - delta, dV role S' = Q K^T - lse2 -> P (bf16, kept + to LDS)
+    f32x16 c[2];
+    bf16x8 sp[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int q0 = qbase + 32 * kb;
+      if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
+      {
+        const float* rowc = (DK ? ds : ls) + 32 * kb + 4 * h;
+        const float4v r0 = *reinterpret_cast<const float4v*>(rowc), r1 = *reinterpret_cast<const float4v*>(rowc + 8),
+                      r2 = *reinterpret_cast<const float4v*>(rowc + 16), r3 = *reinterpret_cast<const float4v*>(rowc + 24);
+        c[kb] = __builtin_shufflevector(__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                        __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4, 5, 6,
+                                        7, 8, 9, 10, 11, 12, 13, 14, 15);
+      }
+      const char* img = DK ? gs : qs;
+      bf16x8 xa[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) xa[s] = lds_row(img, 32 * kb + c32, 2 * s + h);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        bf16x8 xn = xa[s & 1];
+        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
+        __builtin_amdgcn_sched_barrier(0);
+        c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
+        __builtin_amdgcn_sched_barrier(0);
+        xa[s & 1] = xn;
+      }
+      if (!DK) {
+        const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform: only diagonal tiles pay the mask
+        if (tile_mask) {
+          asm volatile("" ::: "memory");
+          const int mthr = key - q0 - 4 * h;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(c[kb][r]);
+            c[kb][r] = mthr > (r & 3) + 8 * (r >> 2) ? 0.f : p;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) c[kb][r] = fast_exp2(c[kb][r]);
+        }
+        sp[kb][0] = pack8(c[kb], 0);
+        sp[kb][1] = pack8(c[kb], 8);
+        pbuf[(2 * kb) * 64 + lane] = sp[kb][0];
+        pbuf[(2 * kb + 1) * 64 + lane] = sp[kb][1];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // P of both pairs visible
+    // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int q0 = qbase + 32 * kb;
+      if (causal && q0 + 31 < k0) continue;
+      bf16x8 s0, s1;
+      if (DK) {
+        const ushort8 p0 = __builtin_bit_cast(ushort8, pbuf[(2 * kb) * 64 + lane]);
+        const ushort8 p1 = __builtin_bit_cast(ushort8, pbuf[(2 * kb + 1) * 64 + lane]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          c[kb][j] = bf2f(p0[j]) * c[kb][j];
+          c[kb][8 + j] = bf2f(p1[j]) * c[kb][8 + j];
+        }
+        s0 = pack8(c[kb], 0);
+        s1 = pack8(c[kb], 8);
+      } else {
+        s0 = sp[kb][0];
+        s1 = sp[kb][1];
+      }
+      const char* op = DK ? qs : gs;
+      bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        bf16x8 n0 = t0, n1 = t1;
+        if (d < 3) {
+          n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
+          n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc[d] = mfma(t0, s0, acc[d]);
+        acc[d] = mfma(t1, s1, acc[d]);
+        __builtin_amdgcn_sched_barrier(0);
+        t0 = n0;
+        t1 = n1;
+      }
+    }
+  }
+  if (key < S) {
+    ushort* orow = out + b * bs + (long)key * ld + (long)hk * HD;
+    const float f = DK ? scale : 1.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        ushort4v o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[d][4 * g + e] * f);
+        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = o;
+      }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void fa_bwd_kh_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+  __shared__ __attribute__((aligned(1024))) char smem[KH_LDS];
+  const int nkb = (S + KH_BK - 1) / KH_BK;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = L / nkb, kb_i = L % nkb;  // (batch, kv head)-major, heaviest key block first
+  const int b = grp / Hkv, hk = grp % Hkv;
+  const int kblk = causal ? kb_i : nkb - 1 - kb_i;
+  const int G = Hq / Hkv;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+  if (threadIdx.x >= 128)
+    kh_body<false>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * KH_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+                   scale_log2, causal);
+  else
+    kh_body<true>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * KH_BK, S, Hq, G, ld, bs, ldo, bso, scale,
+                  scale_log2, causal);
+}
+
 constexpr int B_LDS = 2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4;
 }  // namespace
 
@@ -1367,7 +1599,12 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernel)
   if (!(flags & 8)) {
     const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;
-    if (dq_dma && (flags & 128))  // bit7: one barrier per tile (3-deep Q/dO ring, bf16 P exchange)
+    if (dq_dma && (flags & 256)) {  // bit8: half-width paired kernel, two workgroups per CU
+      const long nkh = (long)((S + KH_BK - 1) / KH_BK) * Hkv * B;
+      fa_bwd_kh_kernel<<<(unsigned)nkh, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                     (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
+                                                     B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+    } else if (dq_dma && (flags & 128))  // bit7: one barrier per tile (3-deep Q/dO ring, bf16 P exchange)
       fa_bwd_kc3_kernel<<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                       (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
                                                       B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
