@@ -476,6 +476,174 @@ def multitenant(jobs_per_user: int = 8, seed: int = 0, duration_s: tuple[float, 
                         f"{duration_s[0]}-{duration_s[1]} s, mean inter-arrival {arrival_s} s"}
 
 
+_NODE_JOB = r"""
+import sys, time, torch
+secs = float(sys.argv[1])
+x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+print("started", torch.cuda.device_count(), flush=True)
+t0, n = time.time(), 0
+while time.time() - t0 < secs:
+    y = x @ x
+    n += 1
+    if n % 32 == 0:
+        torch.cuda.synchronize()
+torch.cuda.synchronize()
+print("done", n, flush=True)
+"""
+
+_NODE_INTRUDER = r"""
+import sys, time, torch
+x = torch.ones(64 << 20, device="cuda"); torch.cuda.synchronize()
+print("ready", flush=True)
+time.sleep(float(sys.argv[1]))
+"""
+
+
+def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[float, float] = (6.0, 10.0),
+                     arrival_s: float = 2.0, gpus_per_job: int | None = None, timeout_s: float = 600.0) -> dict:
+    """BASELINE config 4 on the REAL node, in real time: three users submit GPU jobs to the queue
+    (``HIP_VISIBLE_DEVICES=auto:k``); the daemon's own monitoring (amdsmi + KFD, 0.25 s), job
+    scheduling (gang placement over the node's actual free GPUs) and ``th-run`` launch them as
+    real processes that run bf16 GEMMs on the device until their time is up.  Queue wait is
+    enqueue -> ``th-run`` launch; node utilisation is the share of GPU-samples that hold a job's
+    process (from the telemetry snapshots, not from the harness's own bookkeeping).  Afterwards a
+    foreign process on a GPU that "bob" has reserved is detected by the protection service.
+
+    ``gpus_per_job`` defaults to 2 on a node with >= 2 GPUs (the BASELINE config) and 1 on a
+    one-GPU box.  The simulated, scaled-time variant is :func:`multitenant`."""
+    import random
+
+    from .core.daemon import Daemon
+    from .core.services import JobSchedulingService, MonitoringService, ProtectionService
+    from .core.telemetry import AmdSmiBackend
+    from .database import db_session
+    from .models.orm import CommandSegment, Job, Reservation, Resource, Restriction, Role, SegmentType, Task, User
+    from .native.build import build_all
+    from .utils import dates
+
+    me = getpass.getuser()
+    if me == "root":
+        return {"metric": "multitenant_node", "skipped": "run as an ordinary user"}
+    build_all(strict=False)
+    rng = random.Random(seed)
+    host = "localhost"
+    with sandbox({host: "local"}, job_interval=3600.0) as (cfg, d):
+        smi = AmdSmiBackend()
+        daemon = Daemon(cfg, backends={host: smi}, init_key=False, test_ssh=False)
+        mon = MonitoringService(0.25, {host: smi})
+        mon.inject(daemon)
+        mon.do_run()
+        gpus = daemon.infrastructure.snapshot().data[host]["GPU"]
+        n_gpus = len(gpus)
+        k = gpus_per_job or (2 if n_gpus >= 2 else 1)
+        by_index = {g["index"]: u for u, g in gpus.items()}
+        for u in gpus:
+            Resource(id=u, name="MI355X", hostname=host).save()
+        names = ("alice", "bob", "carol")
+        users = {}
+        g = Restriction(name="everyone", starts_at=dates.utcnow() - timedelta(days=1), is_global=True)
+        g.save()
+        for n in names:
+            users[n] = User(username=n, password="benchmark password", email=f"{n}@example.org",
+                            roles=[Role(name="user")])
+            users[n].save()
+            g.apply_to_user(users[n])
+        script = d / "job.py"
+        script.write_text(_NODE_JOB)
+        seg = CommandSegment(name="HIP_VISIBLE_DEVICES", segment_type=SegmentType.env_variable)
+        seg.save()
+        plan, t = [], 0.0
+        for j in range(jobs_per_user * len(names)):
+            t += rng.expovariate(1.0 / arrival_s)
+            plan.append((t, names[j % len(names)], rng.uniform(*duration_s)))
+        sched = JobSchedulingService(0.25, 5, 30)
+        daemon.add_service(mon)
+        daemon.add_service(sched)
+        mon.start()
+        sched.start()
+        enq: dict[int, float] = {}
+        busy, waiting = [], []
+        t0 = time.time()
+        try:
+            pending = list(plan)
+            last_snap = None
+            while time.time() - t0 < timeout_s:
+                now_s = time.time() - t0
+                while pending and pending[0][0] <= now_s:
+                    _at, n, dur = pending.pop(0)
+                    job = Job(name=f"{n}-{len(enq)}", description="", user_id=users[n].id)
+                    job.save()
+                    tk = Task(command=f"{sys.executable} {script} {dur:.1f}", hostname=host)
+                    tk.save()
+                    tk.add_cmd_segment(seg, f"auto:{k}")
+                    job.add_task(tk)
+                    job.enqueue()
+                    enq[job.id] = time.time()
+                    daemon.wake("enqueue")
+                snap = daemon.infrastructure.snapshot()
+                if snap is not last_snap:  # one utilisation sample per telemetry update
+                    last_snap = snap
+                    gs = snap.data[host]["GPU"].values()
+                    busy.append(sum(1 for x in gs if x.get("processes")))
+                    launched = {jid for jid, _ts in sched.launch_log}
+                    waiting.append(any(jid not in launched for jid in enq))
+                db_session.expire_all()
+                if not pending and enq and all(Job.get(j).status.name not in ("pending", "running")
+                                               for j in enq):
+                    break
+                time.sleep(0.05)
+            makespan = time.time() - t0
+            starts = dict(sched.launch_log)
+        finally:
+            sched.stop()
+        waits = [(starts[j] - enq[j]) * 1e3 for j in enq if j in starts]
+        statuses = {}
+        for j in enq:
+            st = Job.get(j).status.name
+            statuses[st] = statuses.get(st, 0) + 1
+        # violation path on the real device: bob reserves GPU 0, an unscheduled process uses it
+        now = dates.utcnow()
+        Reservation(user_id=users["bob"].id, title="bob-0", description="", resource_id=by_index[0],
+                    start=now - timedelta(minutes=1), end=now + timedelta(hours=1)).save()
+        seen = []
+
+        class _Recorder:
+            def trigger_action(self, data):
+                seen.append(data)
+
+        prot = ProtectionService(0.25, [_Recorder()], level=1)
+        prot.inject(daemon)
+        p = subprocess.Popen([sys.executable, "-c", _NODE_INTRUDER, "30"], stdout=subprocess.PIPE, text=True,
+                             env={**os.environ, "HIP_VISIBLE_DEVICES": "0"})
+        detect_ms = None
+        try:
+            if p.stdout.readline().strip() == "ready":
+                t1 = time.time()
+                while time.time() - t1 < 15 and detect_ms is None:
+                    mon.do_run()
+                    prot.do_run()
+                    if any(p.pid in pids for v in seen for pids in v["VIOLATION_PIDS"].values()):
+                        detect_ms = round((time.time() - t1) * 1e3, 1)
+                    time.sleep(0.1)
+        finally:
+            p.kill()
+            p.wait()
+            daemon.shutdown()
+        hit = next((v for v in seen if any(p.pid in pids for pids in v["VIOLATION_PIDS"].values())), None)
+        return {"metric": "multitenant_node", "real_time": True, "gpus_on_node": n_gpus, "gpus_per_job": k,
+                "jobs": len(enq), "job_status": statuses, "launched": len(waits),
+                "queue_wait_p50_ms": round(_pct(waits, 0.5), 1), "queue_wait_p99_ms": round(_pct(waits, 0.99), 1),
+                "node_gpu_util": round(statistics.fmean(busy) / n_gpus, 3) if busy else None,
+                "gpu_util_while_jobs_wait": (round(statistics.fmean([b for b, w in zip(busy, waiting) if w]) / n_gpus, 3)
+                                             if any(waiting) else None),
+                "telemetry_samples": len(busy), "makespan_s": round(makespan, 1),
+                "violation": None if hit is None else {
+                    "intruder": hit["INTRUDER_USERNAME"], "reserved_by": [r["OWNER_USERNAME"] for r in hit["RESERVATIONS"]],
+                    "detect_ms": detect_ms},
+                "note": f"real node, real time: {jobs_per_user * 3} jobs of {duration_s[0]}-{duration_s[1]} s bf16 GEMM "
+                        f"loops, mean inter-arrival {arrival_s} s, each asking HIP_VISIBLE_DEVICES=auto:{k}"}
+
+
 def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3, bucket_mb: float | None = None,
                      extra: list[str] | None = None) -> dict:
     """Run bench.py (torchrun for gpus>1) and return its JSON line."""

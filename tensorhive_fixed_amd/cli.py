@@ -218,14 +218,17 @@ def doctor():
 @click.option("--requests", default=1000)
 @click.option("--gpus", default=1)
 @click.option("--pinned", is_flag=True, help="multitenant: reference-style pinned device pairs")
+@click.option("--real", is_flag=True, help="multitenant: this node's GPUs, real processes, real time")
 @click.option("--bucket-mb", "bucket_mb", multiple=True, type=float,
               help="scaling: gradient bucket sizes to sweep (repeat the option); train: the bucket size")
-def bench(what, requests, gpus, pinned, bucket_mb):
+def bench(what, requests, gpus, pinned, real, bucket_mb):
     """Benchmarks of BASELINE.md: poll latency, queued-job launch latency, multi-tenant queue
     wait / GPU utilisation, training tokens/s, and its 1/2/4/8-GPU weak-scaling curve."""
     from . import benchmarks
 
-    if what == "multitenant":
+    if what == "multitenant" and real:
+        click.echo(json.dumps(benchmarks.multitenant_node()))
+    elif what == "multitenant":
         click.echo(json.dumps(benchmarks.multitenant(pinned=pinned)))
     elif what == "poll":
         click.echo(json.dumps(benchmarks.poll_latency(requests)))
