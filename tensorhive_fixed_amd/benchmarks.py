@@ -480,7 +480,7 @@ _NODE_JOB = r"""
 import sys, time, torch
 secs = float(sys.argv[1])
 x = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
-print("started", torch.cuda.device_count(), flush=True)
+print("started", torch.cuda.device_count(), repr(time.time()), flush=True)
 t0, n = time.time(), 0
 while time.time() - t0 < secs:
     y = x @ x
@@ -488,7 +488,7 @@ while time.time() - t0 < secs:
     if n % 32 == 0:
         torch.cuda.synchronize()
 torch.cuda.synchronize()
-print("done", n, flush=True)
+print("done", n, repr(time.time()), flush=True)
 """
 
 _NODE_INTRUDER = r"""
@@ -500,7 +500,8 @@ time.sleep(float(sys.argv[1]))
 
 
 def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[float, float] = (6.0, 10.0),
-                     arrival_s: float = 2.0, gpus_per_job: int | None = None, timeout_s: float = 600.0) -> dict:
+                     arrival_s: float = 2.0, gpus_per_job: int | None = None, timeout_s: float = 600.0,
+                     tick_s: float = 30.0) -> dict:
     """BASELINE config 4 on the REAL node, in real time: three users submit GPU jobs to the queue
     (``HIP_VISIBLE_DEVICES=auto:k``); the daemon's own monitoring (amdsmi + KFD, 0.25 s), job
     scheduling (gang placement over the node's actual free GPUs) and ``th-run`` launch them as
@@ -510,9 +511,14 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
     foreign process on a GPU that "bob" has reserved is detected by the protection service.
 
     ``gpus_per_job`` defaults to 2 on a node with >= 2 GPUs (the BASELINE config) and 1 on a
-    one-GPU box.  The simulated, scaled-time variant is :func:`multitenant`."""
+    one-GPU box.  ``tick_s`` is the scheduler's periodic tick, the shipped 30 s by default: a job
+    that waits for a busy device is started by the event wake-ups (enqueue, and the monitoring
+    service's "a device lost its last process"), so ``handoff_*`` -- a job's exit to the next
+    waiting job's launch -- measures those, not the tick.  The simulated, scaled-time variant is
+    :func:`multitenant`."""
     import random
 
+    from .core import task_nursery
     from .core.daemon import Daemon
     from .core.services import JobSchedulingService, MonitoringService, ProtectionService
     from .core.telemetry import AmdSmiBackend
@@ -556,12 +562,13 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
         for j in range(jobs_per_user * len(names)):
             t += rng.expovariate(1.0 / arrival_s)
             plan.append((t, names[j % len(names)], rng.uniform(*duration_s)))
-        sched = JobSchedulingService(0.25, 5, 30)
+        sched = JobSchedulingService(tick_s, 5, 30)
         daemon.add_service(mon)
         daemon.add_service(sched)
         mon.start()
         sched.start()
         enq: dict[int, float] = {}
+        task_of: dict[int, int] = {}
         busy, waiting = [], []
         t0 = time.time()
         try:
@@ -579,6 +586,7 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
                     job.add_task(tk)
                     job.enqueue()
                     enq[job.id] = time.time()
+                    task_of[job.id] = tk.id
                     daemon.wake("enqueue")
                 snap = daemon.infrastructure.snapshot()
                 if snap is not last_snap:  # one utilisation sample per telemetry update
@@ -597,6 +605,25 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
         finally:
             sched.stop()
         waits = [(starts[j] - enq[j]) * 1e3 for j in enq if j in starts]
+        # the jobs' own clocks (task logs): launch -> device ready, and the scheduler's hand-off
+        # (a job's exit -> the next waiting job's launch) on a contended node
+        marks: dict[int, dict] = {}
+        for j, tid in task_of.items():
+            try:
+                lines, _ = task_nursery.fetch_log(host, me, tid)
+            except FileNotFoundError:
+                continue
+            for ln in lines:
+                parts = ln.split()
+                if len(parts) >= 3 and parts[0] in ("started", "done"):
+                    marks.setdefault(j, {})[parts[0]] = float(parts[-1])
+        startup = [(m["started"] - starts[j]) * 1e3 for j, m in marks.items() if "started" in m and j in starts]
+        ends = sorted(m["done"] for m in marks.values() if "done" in m)
+        handoff = []
+        for j in sorted(starts, key=starts.get):
+            prev = [e for e in ends if e <= starts[j]]
+            if prev and enq[j] < prev[-1] and starts[j] - prev[-1] < 60:  # waited for a device a job freed
+                handoff.append((starts[j] - prev[-1]) * 1e3)
         statuses = {}
         for j in enq:
             st = Job.get(j).status.name
@@ -637,11 +664,15 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
                 "gpu_util_while_jobs_wait": (round(statistics.fmean([b for b, w in zip(busy, waiting) if w]) / n_gpus, 3)
                                              if any(waiting) else None),
                 "telemetry_samples": len(busy), "makespan_s": round(makespan, 1),
+                "job_startup_p50_ms": round(_pct(startup, 0.5), 1) if startup else None,
+                "handoff_p50_ms": round(_pct(handoff, 0.5), 1) if handoff else None,
+                "handoff_max_ms": round(max(handoff), 1) if handoff else None,
                 "violation": None if hit is None else {
                     "intruder": hit["INTRUDER_USERNAME"], "reserved_by": [r["OWNER_USERNAME"] for r in hit["RESERVATIONS"]],
                     "detect_ms": detect_ms},
                 "note": f"real node, real time: {jobs_per_user * 3} jobs of {duration_s[0]}-{duration_s[1]} s bf16 GEMM "
-                        f"loops, mean inter-arrival {arrival_s} s, each asking HIP_VISIBLE_DEVICES=auto:{k}"}
+                        f"loops, mean inter-arrival {arrival_s} s, each asking HIP_VISIBLE_DEVICES=auto:{k}; "
+                        f"scheduler tick {tick_s:g} s (starts come from event wake-ups)"}
 
 
 def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3, bucket_mb: float | None = None,

@@ -137,10 +137,14 @@ class Daemon:
             task_nursery.use_transports(None)
 
     def wake(self, reason: str = "") -> None:
-        """Event-driven wake-up of the job scheduler (enqueue, reservation change, job stop)."""
+        """Event-driven wake-up of the job scheduler (enqueue, reservation change, job stop, and
+        ``gpu_freed`` from the monitoring service: a device lost its last process)."""
         s = self.service(JobSchedulingService)
         if s is not None:
-            s.wake()
+            if reason == "gpu_freed":
+                s.device_freed()
+            else:
+                s.wake()
 
     def scheduling_window(self):
         """How long a GPU must stay free before a queued job may take it

@@ -78,6 +78,10 @@ class Service(threading.Thread):
     def do_run(self) -> None:
         raise NotImplementedError
 
+    def next_wait(self, dt: float) -> float:
+        """Seconds to sleep after a tick that took ``dt`` (a wake-up cuts it short)."""
+        return max(0.0, self.interval - dt)
+
     def run(self) -> None:
         while not self._stop_ev.is_set():
             t0 = time.perf_counter()
@@ -90,7 +94,7 @@ class Service(threading.Thread):
             dt = time.perf_counter() - t0
             self.stats.add(dt)
             self.ticks += 1
-            self._wake_ev.wait(max(0.0, self.interval - dt))
+            self._wake_ev.wait(self.next_wait(dt))
             self._wake_ev.clear()
 
 
@@ -101,6 +105,7 @@ class MonitoringService(Service):
         self.backends = backends  # host -> TelemetryBackend
         self._pool = cf.ThreadPoolExecutor(max_workers=max(1, min(32, len(backends))),
                                            thread_name_prefix="th-sample")
+        self._busy: dict[str, set] = {}  # host -> UUIDs that held a process in the last sample
 
     def sample_host(self, host: str) -> None:
         try:
@@ -110,7 +115,15 @@ class MonitoringService(Service):
             entry = None
         if entry is None:
             entry = {"CPU": None, "GPU": None}
+        busy = {u for u, g in ((entry.get("GPU") or {}).items()) if g and g.get("processes")}
+        prev = self._busy.get(host)
+        self._busy[host] = busy
         self.d.infrastructure.publish(host, entry)
+        # A device whose last process exited is free for the queue NOW: wake the job scheduler
+        # instead of leaving the next queued job to its periodic tick (30 s by default, the
+        # reference's only trigger -- core/services/JobSchedulingService.py:44).
+        if prev is not None and entry.get("GPU") is not None and prev - busy:
+            self.d.wake("gpu_freed")
 
     def do_run(self) -> None:
         list(self._pool.map(self.sample_host, list(self.backends)))
@@ -288,6 +301,26 @@ class JobSchedulingService(Service):
         self.scheduler = scheduler or GreedyScheduler(free_window_mins)
         self.stubborn: set[int] = set()
         self.launch_log: list[tuple[int, float]] = []  # (job id, unix time of execute)
+        self._fast_until = 0.0  # monotonic deadline of the post-"device freed" re-checks
+        self._queue_left = 0  # queued jobs the last tick could not start
+
+    # A device that lost its last process (MonitoringService) is usually free for the queue, but
+    # the task's exit can reach th-run's session state a moment after the process left the
+    # device, and then this tick still sees the device claimed.  So after such a wake-up the
+    # service re-checks every FAST_RECHECK_S for up to FAST_WINDOW_S while queued jobs remain,
+    # instead of sleeping for its full interval (30 s by default).
+    FAST_RECHECK_S = 0.5
+    FAST_WINDOW_S = 10.0
+
+    def device_freed(self) -> None:
+        self._fast_until = time.monotonic() + self.FAST_WINDOW_S
+        self.wake()
+
+    def next_wait(self, dt: float) -> float:
+        w = super().next_wait(dt)
+        if self._queue_left and time.monotonic() < self._fast_until:
+            return min(w, self.FAST_RECHECK_S)
+        return w
 
     # ---- helpers
     def occupancy(self) -> dict:
@@ -426,6 +459,7 @@ class JobSchedulingService(Service):
         from ..models.orm import Job
 
         queue = Job.get_job_queue()
+        self._queue_left = len(queue)
         if not queue:
             return
         sched = self.scheduler
@@ -433,8 +467,8 @@ class JobSchedulingService(Service):
             jobs = sched.schedule_jobs(self.eligible(queue), self.gpu_slots(occ), self.gpu_info())
         except TypeError:  # a custom Scheduler with the reference's two-argument signature
             jobs = sched.schedule_jobs(self.eligible(queue), self.gpu_slots(occ))
-        for job in jobs:
-            self._execute(job, (getattr(sched, "placements", None) or {}).get(job.id))
+        started = sum(1 for job in jobs if self._execute(job, (getattr(sched, "placements", None) or {}).get(job.id)))
+        self._queue_left = len(queue) - started
 
     def stop_with_grace(self, job_id: int):
         from ..controllers.job import business_stop

@@ -18,3 +18,7 @@ def test_real_node_queue_runs_every_job_and_flags_the_intruder():
     assert r["telemetry_samples"] > 10 and r["node_gpu_util"] > 0, r
     assert r["violation"] and r["violation"]["reserved_by"] == ["bob"], r
     assert r["violation"]["intruder"] == getpass.getuser(), r
+    # the scheduler ticks every 30 s: queued jobs were started by the "device freed" wake-up
+    if r["gpus_on_node"] == 1:  # three jobs on one device: two of them waited for it
+        assert r["handoff_p50_ms"] is not None, r
+    assert r["handoff_p50_ms"] is None or r["handoff_p50_ms"] < 3000, r

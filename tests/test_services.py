@@ -364,3 +364,42 @@ def test_greedy_scheduler_unit():
     ok, busy, long_enough = J(T("h", "0")), J(T("h", "1")), J(T("h", "2"))
     dup = J(T("h", "0"))
     assert s.schedule_jobs({ok: None, busy: None, long_enough: None, dup: None}, slots) == [ok, long_enough]
+
+
+def test_monitoring_wakes_the_scheduler_when_a_gpu_is_freed(daemon):
+    """A device that loses its last process wakes the job scheduler (queued jobs start at the next
+    telemetry sample, not at the scheduler's periodic tick); a host that stops answering does not."""
+    woken = []
+    daemon.wake = lambda reason="": woken.append(reason)
+    mon = MonitoringService(1.0, daemon.backends)
+    mon.inject(daemon)
+    daemon.stub.add_process("node-a", 3, 4242, "alice")
+    mon.do_run()
+    assert woken == []
+    mon.do_run()
+    assert woken == []  # still busy
+    daemon.stub.clear_processes("node-a")
+    mon.do_run()
+    assert woken == ["gpu_freed"]
+    daemon.stub.add_process("node-a", 3, 4243, "alice")
+    mon.do_run()
+    daemon.stub.down.add("node-a")
+    mon.do_run()
+    assert woken == ["gpu_freed"]
+
+
+def test_device_freed_wake_rechecks_while_jobs_wait(sched):
+    """After a "device freed" wake-up the scheduler re-checks every FAST_RECHECK_S (the exit may
+    reach th-run's state after the process left the device) while queued jobs remain, within the
+    window only; otherwise it sleeps its interval."""
+    sched.interval = 3600.0
+    assert sched.next_wait(0.0) == 3600.0
+    sched._queue_left = 2
+    assert sched.next_wait(0.0) == 3600.0  # no device was freed
+    sched.device_freed()
+    assert sched.next_wait(0.0) == sched.FAST_RECHECK_S
+    sched._queue_left = 0
+    assert sched.next_wait(0.0) == 3600.0  # nothing waits
+    sched._queue_left = 1
+    sched._fast_until = 0.0
+    assert sched.next_wait(0.0) == 3600.0  # window over
