@@ -303,12 +303,14 @@ class JobSchedulingService(Service):
         self.launch_log: list[tuple[int, float]] = []  # (job id, unix time of execute)
         self._fast_until = 0.0  # monotonic deadline of the post-"device freed" re-checks
         self._queue_left = 0  # queued jobs the last tick could not start
+        self._idle_claims = False  # the last tick saw a claimed device without a process
 
     # A device that lost its last process (MonitoringService) is usually free for the queue, but
     # the task's exit can reach th-run's session state a moment after the process left the
     # device, and then this tick still sees the device claimed.  So after such a wake-up the
-    # service re-checks every FAST_RECHECK_S for up to FAST_WINDOW_S while queued jobs remain,
-    # instead of sleeping for its full interval (30 s by default).
+    # service re-checks every FAST_RECHECK_S for up to FAST_WINDOW_S while queued jobs remain or
+    # a claimed device shows no process (its task not yet seen as ended), instead of sleeping for
+    # its full interval (30 s by default).
     FAST_RECHECK_S = 0.5
     FAST_WINDOW_S = 10.0
 
@@ -318,7 +320,7 @@ class JobSchedulingService(Service):
 
     def next_wait(self, dt: float) -> float:
         w = super().next_wait(dt)
-        if self._queue_left and time.monotonic() < self._fast_until:
+        if (self._queue_left or self._idle_claims) and time.monotonic() < self._fast_until:
             return min(w, self.FAST_RECHECK_S)
         return w
 
@@ -511,6 +513,7 @@ class JobSchedulingService(Service):
     def do_run(self) -> None:
         self.refresh_allocations()
         occ = self.occupancy()
+        self._idle_claims = any(not occ.get(h, {}).get(u) for h, u in self.claimed(occ))
         if not self.execute_scheduled(occ):
             self.execute_queued(occ)
         self.stop_scheduled()

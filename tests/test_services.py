@@ -400,6 +400,9 @@ def test_device_freed_wake_rechecks_while_jobs_wait(sched):
     assert sched.next_wait(0.0) == sched.FAST_RECHECK_S
     sched._queue_left = 0
     assert sched.next_wait(0.0) == 3600.0  # nothing waits
+    sched._idle_claims = True
+    assert sched.next_wait(0.0) == sched.FAST_RECHECK_S  # a finished task not yet seen as ended
+    sched._idle_claims = False
     sched._queue_left = 1
     sched._fast_until = 0.0
     assert sched.next_wait(0.0) == 3600.0  # window over
