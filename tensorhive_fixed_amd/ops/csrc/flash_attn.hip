@@ -88,6 +88,33 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
   return r;
 }
 
+// Epilogue of a transposed 32x32 accumulator set (4 tiles = 128 head dims on the accumulator rows,
+// one token per lane column): lane l holds dims 32d + 8g + 0..3 and lane l+32 dims 32d + 8g + 4..7
+// of the same token row, so the plain store is 16 dwordx2 per lane.  One v_permlane32_swap per
+// dword and group pair (g, g+1) gives lanes 0-31 the 16 contiguous bytes of group g and lanes 32-63
+// those of group g+1: 8 dwordx4 stores per lane, same bytes (cdna_hip_programming.md T21: the tail
+// is store-issue-bound).  Both lanes of a pair hold the same token, so a token-validity branch
+// around the call never splits a pair.
+__device__ __forceinline__ void store_row_t21(ushort* row, const f32x16 (&acc)[4], float f, int h) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      unsigned a[2], c[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        a[k] = (unsigned)f2bf(acc[d][8 * p + 2 * k] * f) | ((unsigned)f2bf(acc[d][8 * p + 2 * k + 1] * f) << 16);
+        c[k] = (unsigned)f2bf(acc[d][8 * p + 4 + 2 * k] * f) | ((unsigned)f2bf(acc[d][8 * p + 5 + 2 * k] * f) << 16);
+        const auto r = __builtin_amdgcn_permlane32_swap(a[k], c[k], false, false);
+        a[k] = r[0];
+        c[k] = r[1];
+      }
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = {a[0], a[1], c[0], c[1]};
+      *reinterpret_cast<u32x4*>(row + 32 * d + 16 * p + 8 * h) = v;
+    }
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -395,16 +422,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 
   if (q < S) {
     const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
-    ushort* orow = O + b * bso + (long)q * ldo + (long)hq * HD;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4v out;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) out[e] = f2bf(o[d][4 * g + e] * inv_l);
-        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = out;
-      }
+    store_row_t21(O + b * bso + (long)q * ldo + (long)hq * HD, o, inv_l, h);
     if (h == 0) LSE[((long)b * Hq + hq) * S + q] = (m_i + log2f(l_i)) * LN2;
   }
 }
@@ -598,16 +616,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     }
   }
   if (q < S) {
-    ushort* row = dQ + b * bs + (long)q * ld + (long)hq * HD;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4v out;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) out[e] = f2bf(dq[d][4 * g + e] * scale);
-        *reinterpret_cast<ushort4v*>(row + 32 * d + 8 * g + 4 * h) = out;
-      }
+    store_row_t21(dQ + b * bs + (long)q * ld + (long)hq * HD, dq, scale, h);
   }
 }
 
@@ -1034,17 +1043,7 @@ __device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const usho
     }
   }
   if (key < S) {
-    ushort* orow = out + b * bs + (long)key * ld + (long)hk * HD;
-    const float f = DK ? scale : 1.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4v o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[d][4 * g + e] * f);
-        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = o;
-      }
+    store_row_t21(out + b * bs + (long)key * ld + (long)hk * HD, acc, DK ? scale : 1.f, h);
   }
 }
 
@@ -1237,17 +1236,7 @@ __device__ __forceinline__ void kc3_body(const ushort* __restrict__ Q, const ush
     }
   }
   if (key < S) {
-    ushort* orow = out + b * bs + (long)key * ld + (long)hk * HD;
-    const float f = DK ? scale : 1.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4v o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[d][4 * g + e] * f);
-        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = o;
-      }
+    store_row_t21(out + b * bs + (long)key * ld + (long)hk * HD, acc, DK ? scale : 1.f, h);
   }
 }
 
@@ -1495,17 +1484,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
     }
   }
   if (key < S) {
-    ushort* orow = out + b * bs + (long)key * ld + (long)hk * HD;
-    const float f = DK ? scale : 1.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        ushort4v o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[d][4 * g + e] * f);
-        *reinterpret_cast<ushort4v*>(orow + 32 * d + 8 * g + 4 * h) = o;
-      }
+    store_row_t21(out + b * bs + (long)key * ld + (long)hk * HD, acc, DK ? scale : 1.f, h);
   }
 }
 
