@@ -95,9 +95,10 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 
 
 # launch flags of the backward (th_flash_attn_bwd), A/B aids: bit0 q-major dQ order; bit1 / bit2
-# fused dK/dV order / priority; bit3 the fused dK/dV kernel instead of the paired one; bit5
-# register-staged K/V tiles in dQ (and in dK|dV); bit6 register-staged Q/dO tiles in the paired
-# dK|dV kernel; bit7 the one-barrier-per-tile paired kernel (profiles/r02_flash: slower)
+# fused dK/dV order / priority; bit3 the fused dK/dV kernel instead of a paired one; bit5
+# register-staged K/V tiles in dQ (and in dK|dV); bit6 register-staged Q/dO tiles in the 8-wave
+# paired dK|dV kernel; bit7 its one-barrier-per-tile variant (profiles/r02_flash: slower); bit8 the
+# 8-wave paired kernel instead of the default half-width one (profiles/r03_flash)
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", "0"))
 
 

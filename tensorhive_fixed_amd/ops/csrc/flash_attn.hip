@@ -1575,10 +1575,13 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
     if (dq_dma) TH_DQ_LAUNCH(true, true); else TH_DQ_LAUNCH(true, false);
   }
 #undef TH_DQ_LAUNCH
-  // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernel)
+  // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernels below)
   if (!(flags & 8)) {
     const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;
-    if (dq_dma && (flags & 256)) {  // bit8: half-width paired kernel, two workgroups per CU
+    // default: the half-width paired kernel (two workgroups per CU; step -0.4 % against the 8-wave
+    // one, profiles/r03_flash); bit8: the 8-wave paired kernel (round-2 default); bit7: its
+    // one-barrier variant; bit6 (or bit5 / 32-bit offset overflow): register-staged Q/dO tiles
+    if (dq_dma && !(flags & (256 | 128 | 64))) {
       const long nkh = (long)((S + KH_BK - 1) / KH_BK) * Hkv * B;
       fa_bwd_kh_kernel<<<(unsigned)nkh, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                      (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
