@@ -1399,18 +1399,16 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
     // phase 1: dK role dP' = dO V^T - delta, dV role S' = Q K^T - lse2 -> P (bf16, kept + to LDS)
     f32x16 c[2];
     bf16x8 sp[2][2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int q0 = qbase + 32 * kb;
-      if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
-      {
-        const float* rowc = (DK ? ds : ls) + 32 * kb + 4 * h;
-        const float4v r0 = *reinterpret_cast<const float4v*>(rowc), r1 = *reinterpret_cast<const float4v*>(rowc + 8),
-                      r2 = *reinterpret_cast<const float4v*>(rowc + 16), r3 = *reinterpret_cast<const float4v*>(rowc + 24);
-        c[kb] = __builtin_shufflevector(__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7),
-                                        __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4, 5, 6,
-                                        7, 8, 9, 10, 11, 12, 13, 14, 15);
-      }
+    auto init_c = [&](int kb) {  // -delta (dK role) / -lse2 (dV role) of the half's 32 query rows
+      const float* rowc = (DK ? ds : ls) + 32 * kb + 4 * h;
+      const float4v r0 = *reinterpret_cast<const float4v*>(rowc), r1 = *reinterpret_cast<const float4v*>(rowc + 8),
+                    r2 = *reinterpret_cast<const float4v*>(rowc + 16), r3 = *reinterpret_cast<const float4v*>(rowc + 24);
+      c[kb] = __builtin_shufflevector(__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                      __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4, 5, 6, 7,
+                                      8, 9, 10, 11, 12, 13, 14, 15);
+    };
+    // the half's 8-MFMA chain, row operands read two k-steps ahead; fill(s) runs in MFMA gap s
+    auto chain1 = [&](int kb, auto&& fill) {
       const char* img = DK ? gs : qs;
       bf16x8 xa[2];
 #pragma unroll
@@ -1421,51 +1419,64 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
         if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
         __builtin_amdgcn_sched_barrier(0);
         c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
+        fill(s);
         __builtin_amdgcn_sched_barrier(0);
         xa[s & 1] = xn;
       }
-      if (!DK) {
-        const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform: only diagonal tiles pay the mask
-        if (tile_mask) {
-          asm volatile("" ::: "memory");
-          const int mthr = key - q0 - 4 * h;
+    };
+    auto no_fill = [](int) {};
+    auto publish_p = [&](int kb) {
+      sp[kb][0] = pack8(c[kb], 0);
+      sp[kb][1] = pack8(c[kb], 8);
+      pbuf[(2 * kb) * 64 + lane] = sp[kb][0];
+      pbuf[(2 * kb + 1) * 64 + lane] = sp[kb][1];
+    };
+    // Interleaved dV schedule (both halves live, neither on the diagonal): half 0's exponentials run
+    // two per MFMA gap of half 1's chain instead of between the chains (MI355X_MICROARCH issue
+    // costs: a gap runs ~max(32, sum of its issue costs), the MFMA's own 8 included, and a v_exp
+    // costs 8, so two fit).  Diagonal / partly-skipped tiles keep the plain order.
+    const bool fast1 = !DK && !(causal && qbase < k0 + 31);
+    if (fast1) {
+      init_c(0);
+      init_c(1);
+      chain1(0, no_fill);
+      chain1(1, [&](int s) {
+        c[0][2 * s] = fast_exp2(c[0][2 * s]);
+        c[0][2 * s + 1] = fast_exp2(c[0][2 * s + 1]);
+      });
+      publish_p(0);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float p = fast_exp2(c[kb][r]);
-            c[kb][r] = mthr > (r & 3) + 8 * (r >> 2) ? 0.f : p;
+      for (int r = 0; r < 16; ++r) c[1][r] = fast_exp2(c[1][r]);
+      publish_p(1);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int q0 = qbase + 32 * kb;
+        if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
+        init_c(kb);
+        chain1(kb, no_fill);
+        if (!DK) {
+          const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform: only diagonal tiles pay the mask
+          if (tile_mask) {
+            asm volatile("" ::: "memory");
+            const int mthr = key - q0 - 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float p = fast_exp2(c[kb][r]);
+              c[kb][r] = mthr > (r & 3) + 8 * (r >> 2) ? 0.f : p;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c[kb][r] = fast_exp2(c[kb][r]);
           }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) c[kb][r] = fast_exp2(c[kb][r]);
+          publish_p(kb);
         }
-        sp[kb][0] = pack8(c[kb], 0);
-        sp[kb][1] = pack8(c[kb], 8);
-        pbuf[(2 * kb) * 64 + lane] = sp[kb][0];
-        pbuf[(2 * kb + 1) * 64 + lane] = sp[kb][1];
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // P of both pairs visible
     // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int q0 = qbase + 32 * kb;
-      if (causal && q0 + 31 < k0) continue;
-      bf16x8 s0, s1;
-      if (DK) {
-        const ushort8 p0 = __builtin_bit_cast(ushort8, pbuf[(2 * kb) * 64 + lane]);
-        const ushort8 p1 = __builtin_bit_cast(ushort8, pbuf[(2 * kb + 1) * 64 + lane]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          c[kb][j] = bf2f(p0[j]) * c[kb][j];
-          c[kb][8 + j] = bf2f(p1[j]) * c[kb][8 + j];
-        }
-        s0 = pack8(c[kb], 0);
-        s1 = pack8(c[kb], 8);
-      } else {
-        s0 = sp[kb][0];
-        s1 = sp[kb][1];
-      }
-      const char* op = DK ? qs : gs;
+    const char* op = DK ? qs : gs;
+    auto chain2 = [&](int kb, const bf16x8& s0, const bf16x8& s1, auto&& fill) {
       bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -1477,9 +1488,40 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
         __builtin_amdgcn_sched_barrier(0);
         acc[d] = mfma(t0, s0, acc[d]);
         acc[d] = mfma(t1, s1, acc[d]);
+        fill(d);
         __builtin_amdgcn_sched_barrier(0);
         t0 = n0;
         t1 = n1;
+      }
+    };
+    auto ds_part = [&](int kb, const ushort8& p0, const ushort8& p1, int j0, int j1) {
+#pragma unroll
+      for (int j = j0; j < j1; ++j) {
+        c[kb][j] = bf2f(p0[j]) * c[kb][j];
+        c[kb][8 + j] = bf2f(p1[j]) * c[kb][8 + j];
+      }
+    };
+    if (DK && !(causal && qbase + 31 < k0)) {
+      // both halves live: half 1's dS = P (dP - delta) runs in the MFMA gaps of half 0's dK chain
+      const ushort8 p00 = __builtin_bit_cast(ushort8, pbuf[lane]), p01 = __builtin_bit_cast(ushort8, pbuf[64 + lane]);
+      const ushort8 p10 = __builtin_bit_cast(ushort8, pbuf[128 + lane]), p11 = __builtin_bit_cast(ushort8, pbuf[192 + lane]);
+      ds_part(0, p00, p01, 0, 8);
+      const bf16x8 a0 = pack8(c[0], 0), a1 = pack8(c[0], 8);
+      chain2(0, a0, a1, [&](int d) { ds_part(1, p10, p11, 2 * d, 2 * d + 2); });
+      chain2(1, pack8(c[1], 0), pack8(c[1], 8), no_fill);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int q0 = qbase + 32 * kb;
+        if (causal && q0 + 31 < k0) continue;
+        if (DK) {
+          const ushort8 p0 = __builtin_bit_cast(ushort8, pbuf[(2 * kb) * 64 + lane]);
+          const ushort8 p1 = __builtin_bit_cast(ushort8, pbuf[(2 * kb + 1) * 64 + lane]);
+          ds_part(kb, p0, p1, 0, 8);
+          chain2(kb, pack8(c[kb], 0), pack8(c[kb], 8), no_fill);
+        } else {
+          chain2(kb, sp[kb][0], sp[kb][1], no_fill);
+        }
       }
     }
   }
