@@ -31,7 +31,7 @@ o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
 do = torch.randn_like(o)
 ops = {"fwd": lambda: flash_fwd(qkv, B, S, Hq, Hkv, D), "bwd": lambda: flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)}
 times = {(k, op): [] for k in libs for op in ops}
-for rnd in range(16):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "16"))):
     for k in (("new", "base") if rnd % 2 else ("base", "new")):
         _lib._lib = libs[k]
         for op, fn in ops.items():
