@@ -382,22 +382,18 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         m_i = m_new;
       }
       float rs4[4] = {0.f, 0.f, 0.f, 0.f};  // 4 partial row sums: no 32-deep dependent add chain
+      auto p_of = [&](int kb, int r) {
+        const float p = fast_exp2(SHIFT ? sacc[kb][r] : sacc[kb][r] - m_use);
+        sacc[kb][r] = p;
+        rs4[r & 3] += p;
+      };
+      // keys 0-31 first: their P feeds the first two PV k-steps, and the exponentials of keys 32-63
+      // run two per MFMA gap of those steps instead of ahead of the whole PV chain
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(SHIFT ? sacc[kb][r] : sacc[kb][r] - m_use);
-          sacc[kb][r] = p;
-          rs4[r & 3] += p;
-        }
-      const float rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
-      l_i += half_swap_sum(rs);
+      for (int r = 0; r < 16; ++r) p_of(0, r);
       bf16x8 pf[4];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        pf[2 * kb] = pack8(sacc[kb], 0);
-        pf[2 * kb + 1] = pack8(sacc[kb], 8);
-      }
+      pf[0] = pack8(sacc[0], 0);
+      pf[1] = pack8(sacc[0], 8);
       {  // V^T operands read one k-step ahead
         FA_PRIO(1);
         bf16x8 vt[4];
@@ -405,18 +401,30 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         for (int d = 0; d < 4; ++d) vt[d] = lds_tr(vs, 0, 32 * d, lane);
 #pragma unroll
         for (int ks4 = 0; ks4 < 4; ++ks4) {
+          if (ks4 == 2) {
+            pf[2] = pack8(sacc[1], 0);
+            pf[3] = pack8(sacc[1], 8);
+          }
           bf16x8 nx[4];
 #pragma unroll
           for (int d = 0; d < 4; ++d) nx[d] = ks4 < 3 ? lds_tr(vs, 16 * ks4 + 16, 32 * d, lane) : vt[d];
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int d = 0; d < 4; ++d) o[d] = mfma(vt[d], pf[ks4], o[d]);
+          for (int d = 0; d < 4; ++d) {
+            o[d] = mfma(vt[d], pf[ks4], o[d]);
+            if (ks4 < 2) {
+              p_of(1, 8 * ks4 + 2 * d);
+              p_of(1, 8 * ks4 + 2 * d + 1);
+            }
+          }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int d = 0; d < 4; ++d) vt[d] = nx[d];
         }
         FA_PRIO(0);
       }
+      const float rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
+      l_i += half_swap_sum(rs);
     }
   }
 
