@@ -675,6 +675,80 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
                         f"scheduler tick {tick_s:g} s (starts come from event wake-ups)"}
 
 
+def monitoring_overhead(window_s: float = 20.0, train_rounds: int = 2, steps: int = 8, warmup: int = 3) -> dict:
+    """What the monitoring costs, on the real node (BASELINE: "monitoring overhead"; the reference ran
+    ``nvidia-smi`` plus one SSH round trip per GPU process every 2-5 s, ``core/monitors/GPUMonitor.py``).
+
+    * ``daemon``: a MonitoringService at the shipped 0.25 s cadence over this node's amdsmi backend
+      with the per-GPU ``th-probe`` agent on (the shipped defaults): per-sample wall time, and the CPU
+      time of this process and of the probe agent over ``window_s``, as a share of one core.
+    * ``tenant``: ``bench.py`` tokens/s of a training step started (a) with nothing else running,
+      (b) while that monitoring runs, and (c) with the in-task HBM counter tool (``libthhbm`` through
+      ``ROCP_TOOL_LIBRARIES``, what ``th-run`` injects into every task), alternating ``train_rounds``
+      times in one box."""
+    import psutil
+
+    from .core import hbm
+    from .core.daemon import Daemon
+    from .core.services import MonitoringService
+    from .core.telemetry import AmdSmiBackend
+
+    def bench_once(env_extra: dict | None = None) -> float:
+        env = {**os.environ, **(env_extra or {})}
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", str(steps), "--warmup", str(warmup),
+                            "--daemon-bench", "0"], capture_output=True, text=True, env=env, cwd=ROOT)
+        for line in reversed(r.stdout.splitlines()):
+            if line.startswith("{"):
+                return float(json.loads(line)["value"])
+        raise RuntimeError(f"bench.py failed ({r.returncode}): {r.stderr[-1500:]}")
+
+    out: dict = {"metric": "monitoring_overhead"}
+    with sandbox({"localhost": "local"}, job_interval=3600.0) as (cfg, _d):
+
+        @contextlib.contextmanager
+        def monitoring():
+            """The shipped monitoring of this node: amdsmi sampler at 0.25 s + the th-probe agent."""
+            smi = AmdSmiBackend(probe=True, probe_period=1.0)
+            daemon = Daemon(cfg, backends={"localhost": smi}, init_key=False, test_ssh=False)
+            mon = MonitoringService(0.25, {"localhost": smi})
+            mon.inject(daemon)
+            daemon.add_service(mon)
+            try:
+                mon.do_run()
+                mon.start()
+                yield daemon, mon
+            finally:
+                daemon.shutdown()
+                smi.close()
+
+        me = psutil.Process()
+        with monitoring() as (daemon, mon):
+            time.sleep(2.0)  # the probe agent's first idle references
+            agent = me.children(recursive=True)
+            c0, a0, t0, k0 = me.cpu_times(), sum(sum(c.cpu_times()[:2]) for c in agent), time.time(), mon.ticks
+            time.sleep(window_s)
+            c1, a1, wall = me.cpu_times(), sum(sum(c.cpu_times()[:2]) for c in agent), time.time() - t0
+            snap = daemon.infrastructure.snapshot().data["localhost"]["GPU"] or {}
+            out["daemon"] = {"cadence_s": 0.25, "gpus": len(snap), "samples": mon.ticks - k0, "window_s": round(wall, 1),
+                             "sample_ms": mon.stats.summary(), "helper_processes": len(agent),
+                             "daemon_cpu_pct_of_one_core": round(100 * ((c1.user + c1.system) - (c0.user + c0.system)) / wall, 2),
+                             "probe_agent_cpu_pct_of_one_core": round(100 * (a1 - a0) / wall, 2),
+                             "probe_duty_pct": [g.get("probe_duty") for g in snap.values()]}
+        # tenant impact: alternate (a) nothing else, (b) the monitoring running, (c) the in-task HBM tool
+        rates = {"alone": [], "with_monitoring": [], "with_task_hbm_tool": []}
+        for _ in range(train_rounds):
+            rates["alone"].append(bench_once())
+            with monitoring():
+                rates["with_monitoring"].append(bench_once())
+            rates["with_task_hbm_tool"].append(bench_once(hbm.task_env()))
+        alone = statistics.fmean(rates["alone"])
+        out["tenant"] = {"tokens_per_sec": rates, "bench": f"bench.py --steps {steps} --warmup {warmup}",
+                         "monitoring_cost_pct": round(100 * (1 - statistics.fmean(rates["with_monitoring"]) / alone), 2),
+                         "task_hbm_tool_cost_pct": round(100 * (1 - statistics.fmean(rates["with_task_hbm_tool"]) / alone), 2),
+                         "task_hbm_tool": hbm.tool_path()}
+    return out
+
+
 def train_throughput(gpus: int = 1, steps: int = 10, warmup: int = 3, bucket_mb: float | None = None,
                      extra: list[str] | None = None) -> dict:
     """Run bench.py (torchrun for gpus>1) and return its JSON line."""

@@ -214,7 +214,8 @@ def doctor():
 
 
 @main.command()
-@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled", "multitenant", "scaling"]))
+@click.argument("what", type=click.Choice(["poll", "launch", "train", "scheduled", "multitenant", "scaling",
+                                           "overhead"]))
 @click.option("--requests", default=1000)
 @click.option("--gpus", default=1)
 @click.option("--pinned", is_flag=True, help="multitenant: reference-style pinned device pairs")
@@ -226,7 +227,9 @@ def bench(what, requests, gpus, pinned, real, bucket_mb):
     wait / GPU utilisation, training tokens/s, and its 1/2/4/8-GPU weak-scaling curve."""
     from . import benchmarks
 
-    if what == "multitenant" and real:
+    if what == "overhead":  # monitoring cost on this node: daemon CPU, probe duty, tenant tokens/s
+        click.echo(json.dumps(benchmarks.monitoring_overhead()))
+    elif what == "multitenant" and real:
         click.echo(json.dumps(benchmarks.multitenant_node()))
     elif what == "multitenant":
         click.echo(json.dumps(benchmarks.multitenant(pinned=pinned)))
