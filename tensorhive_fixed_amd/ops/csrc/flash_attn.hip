@@ -1421,6 +1421,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
       bf16x8 xa[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) xa[s] = lds_row(img, 32 * kb + c32, 2 * s + h);
+      FA_PRIO(1);
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         bf16x8 xn = xa[s & 1];
@@ -1431,6 +1432,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
         __builtin_amdgcn_sched_barrier(0);
         xa[s & 1] = xn;
       }
+      FA_PRIO(0);
     };
     auto no_fill = [](int) {};
     auto publish_p = [&](int kb) {
@@ -1486,6 +1488,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
     const char* op = DK ? qs : gs;
     auto chain2 = [&](int kb, const bf16x8& s0, const bf16x8& s1, auto&& fill) {
       bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
+      FA_PRIO(1);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         bf16x8 n0 = t0, n1 = t1;
@@ -1501,6 +1504,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
         t0 = n0;
         t1 = n1;
       }
+      FA_PRIO(0);
     };
     auto ds_part = [&](int kb, const ushort8& p0, const ushort8& p1, int j0, int j1) {
 #pragma unroll
