@@ -459,6 +459,14 @@ __global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict_
 
 
 // ------------------------------------------------------------------------------- dQ kernel
+// dQ: wave priority around the MFMA chains (round 1 measured it neutral on the older dQ body)
+#ifndef TH_DQ_PRIO_ON
+#define TH_DQ_PRIO_ON 1
+#endif
+#define TH_DQ_PRIO(p)                                     \
+  do {                                                    \
+    if (TH_DQ_PRIO_ON) __builtin_amdgcn_s_setprio(p);    \
+  } while (0)
 #ifndef TH_DQ_AHEAD
 #define TH_DQ_AHEAD 1  // 0: reads issued right before their MFMA (compiler order)
 #endif
@@ -558,6 +566,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           ka[s] = lds_row(ks, 32 * kb + c32, 2 * s + h);
           va[s] = lds_row(vs, 32 * kb + c32, 2 * s + h);
         }
+        TH_DQ_PRIO(1);
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           bf16x8 kn = ka[s & 1], vn = va[s & 1];
@@ -572,6 +581,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           ka[s & 1] = kn;
           va[s & 1] = vn;
         }
+        TH_DQ_PRIO(0);
       }
 #else
 #pragma unroll
@@ -599,6 +609,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 #if TH_DQ_AHEAD
       {  // K^T operands one d-step ahead
         bf16x8 t0 = lds_tr(ks, 32 * kb, 0, lane), t1 = lds_tr(ks, 32 * kb + 16, 0, lane);
+        TH_DQ_PRIO(1);
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           bf16x8 n0 = t0, n1 = t1;
@@ -613,6 +624,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           t0 = n0;
           t1 = n1;
         }
+        TH_DQ_PRIO(0);
       }
 #else
 #pragma unroll
