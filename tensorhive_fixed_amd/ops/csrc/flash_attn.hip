@@ -435,29 +435,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   }
 }
 
-// ------------------------------------------------------------------------ delta = rowsum(dO*O)
-__global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict__ O,
-                                                       const ushort* __restrict__ dO,
-                                                       float* __restrict__ delta, int B, int S,
-                                                       int Hq, long ldo, long bso) {
-  const long row = blockIdx.x * 16L + (threadIdx.x >> 4);  // (b, q, hq) flattened, 16 lanes/row
-  const long total = (long)B * S * Hq;
-  if (row >= total) return;
-  const int hq = (int)(row % Hq);
-  const long bq = row / Hq;
-  const int q = (int)(bq % S), b = (int)(bq / S);
-  const long off = b * bso + (long)q * ldo + (long)hq * HD + ((threadIdx.x & 15) << 3);
-  const ushort8 a = *reinterpret_cast<const ushort8*>(O + off);
-  const ushort8 g = *reinterpret_cast<const ushort8*>(dO + off);
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(g[j]);
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
-  if ((threadIdx.x & 15) == 0) delta[((long)b * Hq + hq) * S + q] = s;
-}
-
-
 // ------------------------------------------------------------------------------- dQ kernel
 // dQ: wave priority around the MFMA chains (round 1 measured it neutral on the older dQ body)
 #ifndef TH_DQ_PRIO_ON
@@ -473,9 +450,9 @@ __global__ __launch_bounds__(256) void fa_delta_kernel(const ushort* __restrict_
 template <bool KVMAJOR, bool DMA>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
-    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
-    ushort* __restrict__ dQ, int B, int S, int Hq, int Hkv, long ld, long bs, long ldo, long bso,
-    float scale, float scale_log2, int causal) {
+    const ushort* __restrict__ dO, const ushort* __restrict__ O, const float* __restrict__ LSE,
+    float* __restrict__ Dl, ushort* __restrict__ dQ, int B, int S, int Hq, int Hkv, long ld, long bs, long ldo,
+    long bso, float scale, float scale_log2, int causal) {
   // DMA: two K|V image pairs (64 KB), else one pair staged through registers
   __shared__ __attribute__((aligned(1024))) char smem_dq[(DMA ? 2 : 1) * 2 * F_BN * 256];
   const int nqb = (S + F_BM - 1) / F_BM;
@@ -490,17 +467,28 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   const ushort* Kb = K + b * bs + (long)hk * HD;
   const ushort* Vb = V + b * bs + (long)hk * HD;
   const ushort* dOb = dO + b * bso + (long)hq * HD;
+  const ushort* Ob = O + b * bso + (long)hq * HD;
 
   bf16x8 qf[8], gf[8];
   ushort8 qraw[8];
+  // delta = rowsum(dO * O) of this lane's query, formed here from the dO row the kernel loads anyway
+  // (the two half-waves hold the two halves of the row) and written for the dK|dV kernel -- no
+  // separate delta pass over dO and O
+  float dpart = 0.f;
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     qraw[s] = q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h) : ushort8(0);
-    gf[s] = as_bf(q < S ? *reinterpret_cast<const ushort8*>(dOb + (long)q * ldo + 16 * s + 8 * h) : ushort8(0));
+    const ushort8 graw = q < S ? *reinterpret_cast<const ushort8*>(dOb + (long)q * ldo + 16 * s + 8 * h) : ushort8(0);
+    const ushort8 oraw = q < S ? *reinterpret_cast<const ushort8*>(Ob + (long)q * ldo + 16 * s + 8 * h) : ushort8(0);
+    gf[s] = as_bf(graw);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dpart += bf2f(oraw[e]) * bf2f(graw[e]);
   }
   const long st = ((long)b * Hq + hq) * S;
   const float lse2 = q < S ? LSE[st + q] * LOG2E : INFINITY;
-  const float dlt = q < S ? Dl[st + q] : 0.f;
+  const float dsum = half_swap_sum(dpart);
+  if (q < S && h == 0) Dl[st + q] = dsum;
+  const float dlt = q < S ? dsum : 0.f;
   // Row constants as the initial accumulators (the query is this lane's for the whole kernel): Q is
   // prescaled by softmax_scale * log2(e) once (as the forward's PRESCALE variant does), the S chain
   // starts from -lse2 and the dP chain from -delta, so p = exp2(acc) and dS = p * acc' -- two VALU
@@ -1624,16 +1612,14 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
                                  int flags, hipStream_t s) {
   (void)dq_acc;
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
-  const long rows = (long)B * S * Hq;
-  fa_delta_kernel<<<(unsigned)((rows + 15) / 16), 256, 0, s>>>((const ushort*)o, (const ushort*)dout,
-                                                               delta, B, S, Hq, ldo, bso);
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
   // bit5: register-staged K/V tiles instead of LDS-DMA (also used when 32-bit offsets overflow)
   const bool dq_dma = !(flags & 32) && (long)S * ld * 2 < (1L << 31);
 #define TH_DQ_LAUNCH(KVM, DMA_)                                                                              \
   fa_bwd_dq_kernel<KVM, DMA_><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, \
-                                                           (const ushort*)dout, lse, delta, (ushort*)dq, B, S, Hq, \
+                                                           (const ushort*)dout, (const ushort*)o, lse, delta, (ushort*)dq, \
+                                                           B, S, Hq, \
                                                            Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal)
   if (flags & 1) {
     if (dq_dma) TH_DQ_LAUNCH(false, true); else TH_DQ_LAUNCH(false, false);
