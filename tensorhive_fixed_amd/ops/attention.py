@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as Fn
 
 from . import _lib
-from .rope import rope_inplace
+from .rope import rope_inplace, rope_tables
 
 
 def attention_backend() -> str:
@@ -102,9 +102,17 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", "0"))
 
 
+# TH_FA_ROPE_FUSED=0: the rotary backward of dq / dk as its own in-place pass after the attention
+# backward instead of inside the dQ and dK|dV kernels' epilogues
+_ROPE_FUSED = os.environ.get("TH_FA_ROPE_FUSED", "1") == "1"
+
+
 def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, B: int,
-              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True, flags: int = 0) -> torch.Tensor:
-    """HIP flash attention backward -> dqkv in the packed layout."""
+              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True, flags: int = 0,
+              rope: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+    """HIP flash attention backward -> dqkv in the packed layout.  ``rope`` = the (cos, sin) tables of
+    ``ops/rope.py``: dq and dk come out with the rotary backward already applied (default dK|dV
+    kernel only, ``flags`` 0)."""
     row = qkv.shape[1]
     if not do.is_contiguous():
         do = do.contiguous()
@@ -118,6 +126,15 @@ def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.T
     dq = dqkv.data_ptr()
     dk = dq + Hq * Dh * 2
     dv = dk + Hkv * Dh * 2
+    if rope is not None:
+        cos, sin = rope
+        if cos.shape != (S, Dh // 2) or cos.dtype != torch.float32 or not cos.is_contiguous():
+            raise ValueError("flash_bwd: rope tables must be contiguous f32 [S, Dh/2]")
+        _lib.call("th_flash_attn_bwd_rope", q, k, v, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                  delta.data_ptr(), dq, dk, dv, B, S, Hq, Hkv, Dh, int(causal), row,
+                  S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), cos.data_ptr(), sin.data_ptr(), int(flags),
+                  _lib.stream_ptr(qkv.device))
+        return dqkv
     _lib.call("th_flash_attn_bwd", q, k, v, o.data_ptr(), do.data_ptr(), lse.data_ptr(),
               delta.data_ptr(), None, dq, dk, dv, B, S, Hq, Hkv, Dh, int(causal), row,
               S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh), int(flags), _lib.stream_ptr(qkv.device))
@@ -148,6 +165,10 @@ class _QKVAttention(torch.autograd.Function):
         B, S, Hq, Hkv, Dh, theta = ctx.dims
         if ctx.backend == "hip" and do.is_cuda:
             qkv, o, lse = ctx.saved_tensors
+            if _ROPE_FUSED and _BWD_FLAGS == 0 and Dh == 128:  # rotary backward inside the kernels
+                tabs = rope_tables(S, Dh, theta, do.device)
+                return (flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh, flags=_BWD_FLAGS, rope=tabs),
+                        None, None, None, None, None, None, None)
             dqkv = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh, flags=_BWD_FLAGS)
         else:
             (qkv,) = ctx.saved_tensors

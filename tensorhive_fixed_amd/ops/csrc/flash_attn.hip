@@ -115,6 +115,30 @@ __device__ __forceinline__ void store_row_t21(ushort* row, const f32x16 (&acc)[4
     }
 }
 
+// Rotary-embedding backward folded into a q / k gradient's epilogue (Llama rotate-half pairs (i, i + 64),
+// the inverse rotation; tables [S][64] f32 as ops/rope.py builds them): lane (c32, h) holds dims
+// 32d + 8g + 4h + e of its row in acc[d][4g + e], so the partner of a dim in blocks 0-1 sits in blocks
+// 2-3 of the same lane and the rotation needs no data exchange.  Replaces the separate in-place
+// rope pass over dQ and dK after the backward.
+__device__ __forceinline__ void rope_bwd_rows(f32x16 (&a)[4], const float* __restrict__ rcos,
+                                              const float* __restrict__ rsin, int pos, int h) {
+  const float* cr = rcos + (long)pos * 64;
+  const float* sr = rsin + (long)pos * 64;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4v c4 = *reinterpret_cast<const float4v*>(cr + 32 * d + 8 * g + 4 * h);
+      const float4v s4 = *reinterpret_cast<const float4v*>(sr + 32 * d + 8 * g + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = a[d][4 * g + e], y = a[d + 2][4 * g + e];
+        a[d][4 * g + e] = x * c4[e] + y * s4[e];
+        a[d + 2][4 * g + e] = y * c4[e] - x * s4[e];
+      }
+    }
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -452,7 +476,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const ushort* __restrict__ O, const float* __restrict__ LSE,
     float* __restrict__ Dl, ushort* __restrict__ dQ, int B, int S, int Hq, int Hkv, long ld, long bs, long ldo,
-    long bso, float scale, float scale_log2, int causal) {
+    long bso, float scale, float scale_log2, int causal, const float* __restrict__ rcos,
+    const float* __restrict__ rsin) {
   // DMA: two K|V image pairs (64 KB), else one pair staged through registers
   __shared__ __attribute__((aligned(1024))) char smem_dq[(DMA ? 2 : 1) * 2 * F_BN * 256];
   const int nqb = (S + F_BM - 1) / F_BM;
@@ -624,6 +649,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     }
   }
   if (q < S) {
+    if (rcos != nullptr) {  // rotary backward in the epilogue (position = the query's index in its sequence)
+      rope_bwd_rows(dq, rcos, rsin, q, h);
+    }
     store_row_t21(dQ + b * bs + (long)q * ld + (long)hq * HD, dq, scale, h);
   }
 }
@@ -1312,7 +1340,8 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
                                         const float* __restrict__ LSE, const float* __restrict__ Dl,
                                         const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
                                         char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
-                                        long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+                                        long bs, long ldo, long bso, float scale, float scale_log2, int causal,
+                                        const float* __restrict__ rcos, const float* __restrict__ rsin) {
   // role-local ids: waves 0-1 are the dK role, 2-3 the dV role of the same 64 keys
   const int tid = threadIdx.x & 127, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
   // P exchange of pair w: [half][s0 | s1][lane] bf16x8, 4 KB
@@ -1538,6 +1567,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
     }
   }
   if (key < S) {
+    if (DK && rcos != nullptr) rope_bwd_rows(acc, rcos, rsin, key, h);  // dK rows: rotary backward
     store_row_t21(out + b * bs + (long)key * ld + (long)hk * HD, acc, DK ? scale : 1.f, h);
   }
 }
@@ -1546,7 +1576,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_kh_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
-    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal, const float* __restrict__ rcos,
+    const float* __restrict__ rsin) {
   __shared__ __attribute__((aligned(1024))) char smem[KH_LDS];
   const int nkb = (S + KH_BK - 1) / KH_BK;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -1558,10 +1589,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_kh_kernel(
   const ushort* Vb = V + b * bs + (long)hk * HD;
   if (threadIdx.x >= 128)
     kh_body<false>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * KH_BK, S, Hq, G, ld, bs, ldo, bso, scale,
-                   scale_log2, causal);
+                   scale_log2, causal, nullptr, nullptr);
   else
     kh_body<true>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * KH_BK, S, Hq, G, ld, bs, ldo, bso, scale,
-                  scale_log2, causal);
+                  scale_log2, causal, rcos, rsin);
 }
 
 constexpr int B_LDS = 2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4;
@@ -1605,13 +1636,15 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   TH_CHECK_LAUNCH();
 }
 
-extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
-                                 const void* dout, const float* lse, float* delta, float* dq_acc,
-                                 void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv, int D,
-                                 int causal, long ld, long bs, long ldo, long bso, float scale,
-                                 int flags, hipStream_t s) {
-  (void)dq_acc;
+// rcos / rsin (the [S][64] rotary tables, or null): the rotary backward of dQ and dK is applied in the
+// dQ and dK|dV kernels' epilogues (default dK|dV kernel only: other flags return -3 with tables given)
+static int flash_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                          const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq,
+                          int Hkv, int D, int causal, long ld, long bs, long ldo, long bso, float scale,
+                          const float* rcos, const float* rsin, int flags, hipStream_t s) {
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
+  if (rcos != nullptr && ((flags & (8 | 32 | 64 | 128 | 256)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
+    return -3;
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
   // bit5: register-staged K/V tiles instead of LDS-DMA (also used when 32-bit offsets overflow)
@@ -1620,7 +1653,8 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
   fa_bwd_dq_kernel<KVM, DMA_><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, \
                                                            (const ushort*)dout, (const ushort*)o, lse, delta, (ushort*)dq, \
                                                            B, S, Hq, \
-                                                           Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal)
+                                                           Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, \
+                                                           rcos, rsin)
   if (flags & 1) {
     if (dq_dma) TH_DQ_LAUNCH(false, true); else TH_DQ_LAUNCH(false, false);
   } else {
@@ -1637,7 +1671,8 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
       const long nkh = (long)((S + KH_BK - 1) / KH_BK) * Hkv * B;
       fa_bwd_kh_kernel<<<(unsigned)nkh, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                      (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
-                                                     B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
+                                                     B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal,
+                                                     rcos, rsin);
     } else if (dq_dma && (flags & 128))  // bit7: one barrier per tile (3-deep Q/dO ring, bf16 P exchange)
       fa_bwd_kc3_kernel<<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
                                                       (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
@@ -1671,4 +1706,24 @@ extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, co
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
         (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, !(flags & 4));
   TH_CHECK_LAUNCH();
+}
+
+extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
+                                 const void* dout, const float* lse, float* delta, float* dq_acc,
+                                 void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv, int D,
+                                 int causal, long ld, long bs, long ldo, long bso, float scale,
+                                 int flags, hipStream_t s) {
+  (void)dq_acc;
+  return flash_bwd_impl(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, causal, ld, bs, ldo, bso,
+                        scale, nullptr, nullptr, flags, s);
+}
+
+// The same backward with the rotary backward of dQ / dK folded into the kernels (ops/attention.py)
+extern "C" int th_flash_attn_bwd_rope(const void* q, const void* k, const void* v, const void* o,
+                                      const void* dout, const float* lse, float* delta, void* dq, void* dk,
+                                      void* dv, int B, int S, int Hq, int Hkv, int D, int causal, long ld,
+                                      long bs, long ldo, long bso, float scale, const float* rcos,
+                                      const float* rsin, int flags, hipStream_t s) {
+  return flash_bwd_impl(q, k, v, o, dout, lse, delta, dq, dk, dv, B, S, Hq, Hkv, D, causal, ld, bs, ldo, bso,
+                        scale, rcos, rsin, flags, s);
 }

@@ -124,3 +124,24 @@ def test_flash_long_sequences_match_fp32(S, Hq, Hkv, bwd_flags):
             rel = ((dqkv[:, cols].float() - ref).norm() / (ref.norm() + 1e-6)).item()
             assert rel < 2e-2, f"group {kv} {name} rel err {rel}"
         del x, q, k, v, s, p, og, g
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 8, 2), (2, 200, 4, 4), (1, 4096, 32, 8)])
+def test_rotary_backward_in_the_kernels_matches_the_separate_pass(B, S, Hq, Hkv):
+    """The rotary backward folded into the dQ / dK epilogues gives the dqkv of the flash backward
+    followed by the separate in-place rope pass (dq, dk rotated; dv untouched)."""
+    from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
+    from tensorhive_fixed_amd.ops.rope import rope_inplace, rope_tables
+
+    torch.manual_seed(7)
+    D = 128
+    qkv = (torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda") * 0.5).to(torch.bfloat16)
+    rope_inplace(qkv, S, Hq + Hkv, D, 500000.0, 1.0)
+    o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
+    do = torch.randn_like(o)
+    ref = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)
+    rope_inplace(ref, S, Hq + Hkv, D, 500000.0, -1.0)
+    got = flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D, rope=rope_tables(S, D, 500000.0, qkv.device))
+    err = ((got.float() - ref.float()).norm() / ref.float().norm()).item()
+    assert err < 5e-3, err  # one bf16 rounding less on the fused path
+    assert torch.equal(got[:, (Hq + Hkv) * D:], ref[:, (Hq + Hkv) * D:])  # dv is not rotated
