@@ -25,6 +25,10 @@ def open_lib(path):
 
 
 libs = {"new": _lib.load(), "base": open_lib(os.environ["AB_BASE_LIB"])}
+# AB_VARIANTS="name=path,...": more builds timed in the same rotation (each reported against base)
+for spec in filter(None, os.environ.get("AB_VARIANTS", "").split(",")):
+    name, path = spec.split("=", 1)
+    libs[name] = open_lib(path)
 B, S, Hq, Hkv, D = int(os.environ.get("FA_B", "8")), 4096, 32, 8, 128
 qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
 o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
@@ -32,7 +36,8 @@ do = torch.randn_like(o)
 ops = {"fwd": lambda: flash_fwd(qkv, B, S, Hq, Hkv, D), "bwd": lambda: flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, D)}
 times = {(k, op): [] for k in libs for op in ops}
 for rnd in range(int(os.environ.get("AB_ROUNDS", "16"))):
-    for k in (("new", "base") if rnd % 2 else ("base", "new")):
+    names = list(libs)
+    for k in (names if rnd % 2 else names[::-1]):
         _lib._lib = libs[k]
         for op, fn in ops.items():
             fn()
@@ -48,5 +53,7 @@ for op in ops:
     for k in libs:
         row[k + "_ms_median"] = round(statistics.median(times[(k, op)]), 4)
         row[k + "_ms_min"] = round(min(times[(k, op)]), 4)
-    row["new_vs_base"] = round(row["base_ms_median"] / row["new_ms_median"], 4)
+    for k in libs:
+        if k != "base":
+            row[k + "_vs_base"] = round(row["base_ms_median"] / row[k + "_ms_median"], 4)
     print(json.dumps(row), flush=True)

@@ -1333,6 +1333,16 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
 // different barrier domains, as in the dQ kernel (60.5 % busy).  LDS per workgroup: two Q|dO
 // tiles (DMA double buffer) + the P exchange of the two pairs, as bf16 (the value the dV MFMA
 // consumes): 2 x 33 KB + 8 KB = 73 KB, two workgroups = 146 KB of the 160 KB.
+#ifndef TH_KH_EXPERIMENT
+#define TH_KH_EXPERIMENT 0  // timing probes (bit0 no P barrier, bit1 no exponentials, bit2 no LDS operand
+                            // reads after the first, bit3 no Q|dO DMA after the first tile, bit4 no wait for
+                            // the DMA at the tile barrier); results wrong
+#endif
+#if TH_KH_EXPERIMENT & 2
+#define KH_EXP2(x) (x)
+#else
+#define KH_EXP2(x) fast_exp2(x)
+#endif
 constexpr int KH_BK = 64, KH_LDS = 2 * KC_TILE + 2 * 4096;
 
 template <bool DK>
@@ -1419,11 +1429,15 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
   }
   for (int it = 0; it < total; ++it) {
     char* cur = smem + (it & 1) * KC_TILE;
+#if TH_KH_EXPERIMENT & 16  // timing probe: the tile barrier without waiting for the DMA
+    asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
+#else
     wait_dma_barrier();  // tile it landed; every wave is past tile it-1 (its buffer is free)
+#endif
     if (it + 1 < total) {
       write_ld((it + 1) & 1);
       adv(pf_h, pf_t);
-      dma_tile(pf_h, pf_t, (it + 1) & 1);
+      if (!(TH_KH_EXPERIMENT & 8)) dma_tile(pf_h, pf_t, (it + 1) & 1);
       adv(lh, lt);
       if (it + 2 < total) load_ld(lh, lt);
     }
@@ -1454,7 +1468,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         bf16x8 xn = xa[s & 1];
-        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
+        if (!(TH_KH_EXPERIMENT & 4) && s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
         __builtin_amdgcn_sched_barrier(0);
         c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
         fill(s);
@@ -1480,12 +1494,12 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
       init_c(1);
       chain1(0, no_fill);
       chain1(1, [&](int s) {
-        c[0][2 * s] = fast_exp2(c[0][2 * s]);
-        c[0][2 * s + 1] = fast_exp2(c[0][2 * s + 1]);
+        c[0][2 * s] = KH_EXP2(c[0][2 * s]);
+        c[0][2 * s + 1] = KH_EXP2(c[0][2 * s + 1]);
       });
       publish_p(0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) c[1][r] = fast_exp2(c[1][r]);
+      for (int r = 0; r < 16; ++r) c[1][r] = KH_EXP2(c[1][r]);
       publish_p(1);
     } else {
 #pragma unroll
@@ -1501,18 +1515,22 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
             const int mthr = key - q0 - 4 * h;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const float p = fast_exp2(c[kb][r]);
+              const float p = KH_EXP2(c[kb][r]);
               c[kb][r] = mthr > (r & 3) + 8 * (r >> 2) ? 0.f : p;
             }
           } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) c[kb][r] = fast_exp2(c[kb][r]);
+            for (int r = 0; r < 16; ++r) c[kb][r] = KH_EXP2(c[kb][r]);
           }
           publish_p(kb);
         }
       }
     }
+#if TH_KH_EXPERIMENT & 1  // timing probe only (wrong results): no P-exchange barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // P of both pairs visible
+#endif
     // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
     const char* op = DK ? qs : gs;
     auto chain2 = [&](int kb, const bf16x8& s0, const bf16x8& s1, auto&& fill) {
@@ -1521,7 +1539,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         bf16x8 n0 = t0, n1 = t1;
-        if (d < 3) {
+        if (!(TH_KH_EXPERIMENT & 4) && d < 3) {
           n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
           n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
         }
