@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
 #ifndef TH_KH_EXPERIMENT
 #define TH_KH_EXPERIMENT 0  // timing probes (bit0 no P barrier, bit1 no exponentials, bit2 no LDS operand
                             // reads after the first, bit3 no Q|dO DMA after the first tile, bit4 no wait for
-                            // the DMA at the tile barrier); results wrong
+                            // the DMA at the tile barrier, bit5 contiguous DMA sources); results wrong
 #endif
 #if TH_KH_EXPERIMENT & 2
 #define KH_EXP2(x) (x)
@@ -1389,8 +1389,12 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
     const unsigned img = lds0 + buf * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 8192;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
+#if TH_KH_EXPERIMENT & 32  // timing probe: each piece reads 1 KB of contiguous bytes from the tile's first row on
+      glds16(base, (unsigned)(min(qq0, S - 1) * ldx) * 2u + (unsigned)(u * 1024 + lane * 16), img + u * 1024);
+#else
       const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
       glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
+#endif
     }
   };
   float lr = 0.f, dr = 0.f;
