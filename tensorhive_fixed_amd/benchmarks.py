@@ -602,6 +602,9 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
                 time.sleep(0.05)
             makespan = time.time() - t0
             starts = dict(sched.launch_log)
+        except BaseException:
+            daemon.shutdown()  # the monitoring thread too; the normal path shuts down after the violation check
+            raise
         finally:
             sched.stop()
         waits = [(starts[j] - enq[j]) * 1e3 for j in enq if j in starts]
