@@ -21,6 +21,8 @@ import subprocess
 import threading
 import time
 
+from ..utils.proc import StderrTail
+
 log = logging.getLogger(__name__)
 
 MOPS_FLOP = 512.0
@@ -88,6 +90,7 @@ class CounterStream:
         except OSError as e:
             self.error = str(e)
             return
+        err = StderrTail(self._proc.stderr, name="th-counters")
         for line in self._proc.stdout:  # type: ignore[union-attr]
             if self._stop.is_set():
                 break
@@ -102,8 +105,13 @@ class CounterStream:
             with self._lock:
                 self._latest = metrics
                 self._raw = doc
-        if self._proc.poll() not in (None, 0) and self.error is None:
-            self.error = (self._proc.stderr.read() or "").strip()[-500:]  # type: ignore[union-attr]
+        if self._proc.wait() != 0 and self.error is None and not self._stop.is_set():
+            self.error = err.text() or f"th-counters exited ({self._proc.returncode})"
+
+    @property
+    def pid(self) -> int | None:
+        """The sampler's pid (the monitor keeps it off every GPU's process list)."""
+        return self._proc.pid if self._proc is not None else None
 
     def latest(self) -> dict:
         with self._lock:

@@ -27,6 +27,8 @@ import time
 import uuid as uuidlib
 from pathlib import Path
 
+from ..utils.proc import StderrTail
+
 log = logging.getLogger(__name__)
 
 NATIVE_LIB = Path(__file__).resolve().parent.parent / "native" / "lib" / "libthsmi.so"
@@ -130,6 +132,8 @@ class AmdSmiBackend(TelemetryBackend):
             return json.loads(self._buf.value[:n].decode("utf-8", "replace"))
 
     def sample(self, host: str) -> dict | None:
+        if self.probe is not None:
+            self.probe.ensure_running()
         self._sync_ignored()  # a helper may have (re)started since the last sample
         doc = self._call(self.lib.thsmi_sample_json)
         own = self.self_pids()
@@ -234,14 +238,22 @@ class GpuProbe:
         self._derived_ts = None
         self._lock = threading.Lock()
         self.error: str | None = None
+        self.restarts = 0
+        self._closed = False
+        self._start()
+
+    def _start(self) -> None:
+        self._started = time.monotonic()
         self._proc = subprocess.Popen(self.cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                                       bufsize=1)
         self.pid = self._proc.pid
-        self._thread = threading.Thread(target=self._read, name="th-probe", daemon=True)
+        self._err = StderrTail(self._proc.stderr, name="th-probe")
+        self._thread = threading.Thread(target=self._read, args=(self._proc, self._err), name="th-probe",
+                                        daemon=True)
         self._thread.start()
 
-    def _read(self) -> None:
-        for line in self._proc.stdout:  # type: ignore[union-attr]
+    def _read(self, proc: subprocess.Popen, err: StderrTail) -> None:
+        for line in proc.stdout:  # type: ignore[union-attr]
             try:
                 doc = json.loads(line)
             except json.JSONDecodeError:
@@ -251,9 +263,22 @@ class GpuProbe:
                 continue
             with self._lock:
                 self._latest = doc
-        rc = self._proc.wait()
-        if rc not in (0, -15) and self.error is None:
-            self.error = f"th-probe exited ({rc}): " + (self._proc.stderr.read() or "").strip()[-300:]  # type: ignore[union-attr]
+        rc = proc.wait()
+        if rc not in (0, -15) and not self._closed:
+            self.error = f"th-probe exited ({rc}): " + err.text(limit=300)
+
+    def ensure_running(self, backoff_s: float = 30.0) -> bool:
+        """Restart an agent that died (driver reset, OOM kill), at most once per ``backoff_s``.
+        The new pid reaches libthsmi's ignore list on the monitor's next sample.  Returns whether a
+        restart happened."""
+        if self._closed or self._proc.poll() is None or time.monotonic() - self._started < backoff_s:
+            return False
+        log.warning("th-probe agent exited (%s); restarting", self.error or self._proc.returncode)
+        with self._lock:
+            self._latest = None
+        self.restarts += 1
+        self._start()
+        return True
 
     def latest(self) -> dict | None:
         with self._lock:
@@ -314,6 +339,7 @@ class GpuProbe:
         return {k: dict(v) for k, v in out.items()}
 
     def close(self) -> None:
+        self._closed = True
         if self._proc.poll() is None:
             self._proc.terminate()
             try:

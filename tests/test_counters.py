@@ -42,3 +42,19 @@ def test_counter_stream_reports_errors(tmp_path):
         assert cs.wait_first(5) is False and cs.error == "no GPU agent"
     finally:
         cs.close()
+
+
+def test_counter_stream_exposes_its_pid_for_the_ignore_list(tmp_path):
+    fake = tmp_path / "th-counters"
+    fake.write_text("#!/bin/sh\nexec sleep 5\n")
+    fake.chmod(fake.stat().st_mode | stat.S_IEXEC)
+    cs = CounterStream(binary=str(fake))
+    try:
+        for _ in range(100):
+            if cs.pid:
+                break
+            import time
+            time.sleep(0.05)
+        assert cs.pid and os.path.exists(f"/proc/{cs.pid}")
+    finally:
+        cs.close()

@@ -69,3 +69,41 @@ def test_probe_stream_derives_per_gpu_metrics(tmp_path):
         assert last[0]["probe_duty"]["value"] == round(100 * 30e-6 / 0.1, 4)  # (10+20) us per 100 ms
     finally:
         probe.close()
+
+
+FLOOD = textwrap.dedent("""
+    import json, sys, time
+    sys.stderr.write("x" * 1023 + "\\n" * 1)
+    for _ in range(400):  # 400 KiB of stderr: a pipe nobody reads would block the agent here
+        sys.stderr.write("w" * 1023 + "\\n")
+    sys.stderr.flush()
+    print(json.dumps({"ts_ns": 1, "period_ms": 100, "gpus": []}), flush=True)
+    time.sleep(30)
+""")
+
+
+def test_agent_stderr_is_drained(tmp_path):
+    f = tmp_path / "flood.py"
+    f.write_text(FLOOD)
+    probe = GpuProbe(period=0.1, cmd=[sys.executable, str(f)])
+    try:
+        assert probe.wait_first(15), "agent blocked on a full stderr pipe"
+    finally:
+        probe.close()
+
+
+def test_dead_agent_is_restarted_with_backoff(tmp_path):
+    f = tmp_path / "crash.py"
+    f.write_text("import sys\nsys.stderr.write('device lost\\n')\nsys.exit(3)\n")
+    probe = GpuProbe(period=0.1, cmd=[sys.executable, str(f)])
+    try:
+        probe._proc.wait(10)
+        probe._thread.join(10)
+        assert probe.error.startswith("th-probe exited (3)") and "device lost" in probe.error
+        first = probe.pid
+        assert probe.ensure_running(backoff_s=3600) is False  # within the backoff window
+        assert probe.ensure_running(backoff_s=0.0) is True
+        assert probe.restarts == 1 and probe.pid != first
+    finally:
+        probe.close()
+    assert probe.ensure_running(backoff_s=0.0) is False  # closed: never restarted
