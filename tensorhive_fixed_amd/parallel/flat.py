@@ -321,11 +321,65 @@ class FlatAdamW:
             torch.cuda.current_stream(self.store.device).wait_event(self.done)
             self.done = None
 
+    @staticmethod
+    def _merge(run: tuple | None, seg: tuple, same_wd: bool = True) -> tuple | None:
+        """``run`` extended by ``seg`` when both are contiguous in the flat AND the local (state)
+        index space (and share the weight decay), else None.  Segments are (flat_lo, flat_hi,
+        local_lo, wd)."""
+        if run is None:
+            return seg
+        a, b, l0, wd = run
+        a2, b2, l2, wd2 = seg
+        if same_wd and wd2 != wd:
+            return None
+        if a2 == b and l2 == l0 + (b - a):
+            return (a, b2, l0, wd)
+        if b2 == a and l2 + (b2 - a2) == l0:
+            return (a2, b, l2, wd)
+        return None
+
+    def _launch_groups(self) -> list[tuple[tuple, list[int]]]:
+        """AdamW launches in forward order: ``[(segment run, bucket indices it completes)]``.
+
+        ``TH_OPT_GROUP_MPARAMS`` (millions of parameters, default 0 = one launch per bucket segment)
+        lets launches cover several flat-contiguous buckets: the streaming kernel runs closer to the
+        HBM ceiling on larger ranges (``profiles/r02_streaming/``), at the price of a coarser
+        per-bucket hand-off to the next forward / all-gather."""
+        limit = int(float(os.environ.get("TH_OPT_GROUP_MPARAMS", "0")) * 1e6)
+        out: list[tuple[tuple, list[int]]] = []
+        run, buckets = None, []
+        for bi in reversed(range(len(self.bucket_segments))):
+            for si in self.bucket_segments[bi]:
+                seg = self.segments[si]
+                merged = self._merge(run, seg) if limit > 0 else None
+                if merged is not None and merged[1] - merged[0] <= limit:
+                    run = merged
+                else:
+                    if run is not None:
+                        out.append((run, buckets))
+                    run, buckets = seg, []
+            if run is None:  # a bucket this rank owns nothing of
+                out.append((None, [bi]))
+            else:
+                buckets.append(bi)
+        if run is not None:
+            out.append((run, buckets))
+        return out
+
     def _step(self, lr: float) -> None:
         st = self.store
         scale = 1.0 / st.world
+        groups = self._launch_groups()
         if self.clip > 0:
-            for i, (a, b, _, _) in enumerate(self.segments):
+            # ||g||^2 over maximal flat-contiguous runs (the sum does not care about decay groups)
+            runs: list[tuple] = []
+            for seg in self.segments:
+                m = self._merge(runs[-1], seg, same_wd=False) if runs else None
+                if m is not None and m[1] - m[0] <= (1 << 31) - 8:
+                    runs[-1] = m
+                else:
+                    runs.append(seg)
+            for i, (a, b, _, _) in enumerate(runs):
                 grad_sumsq_(st.grad_buf[a:b], self.norm_sq, accumulate=i > 0)
             if not self.segments:
                 self.norm_sq.zero_()
@@ -333,18 +387,19 @@ class FlatAdamW:
                 dist.all_reduce(self.norm_sq, op=dist.ReduceOp.SUM, group=st.pg)
         # forward order (last bucket first): in sharded mode each bucket's all-gather starts right after
         # its slice is updated, overlapping the remaining AdamW launches and then the next forward
-        for bi in reversed(range(len(self.bucket_segments))):
-            for si in self.bucket_segments[bi]:
-                a, b, l0, wd = self.segments[si]
+        for run, buckets in groups:
+            if run is not None:
+                a, b, l0, wd = run
                 l1 = l0 + (b - a)
                 adamw_flat_(st.param_buf[a:b], self.master[l0:l1], self.exp_avg[l0:l1], self.exp_avg_sq[l0:l1],
                             st.grad_buf[a:b], lr=lr, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                             weight_decay=wd, step=self.step_count, grad_scale=scale,
                             norm_sq=self.norm_sq if self.clip > 0 else None, clip=self.clip)
-            if st.sharded:
-                st.gather_bucket(bi)
-            elif self.overlap:
-                st.mark_updated(bi)
+            for bi in buckets:
+                if st.sharded:
+                    st.gather_bucket(bi)
+                elif self.overlap:
+                    st.mark_updated(bi)
 
     def grad_norm(self) -> float:
         """Global gradient norm of the last step (forces a host sync; for logging only)."""

@@ -220,3 +220,29 @@ def test_bf16_gradient_path_error_vs_f32_at_world8_accum4(tmp_path):
     # every rank holds the same reduced gradient in the f32 path
     g7 = torch.load(tmp_path / f"prec_rank{world - 1}.pt", weights_only=True)
     assert torch.equal(g7["torch.float32"], f32)
+
+
+@pytest.mark.parametrize("mparams", ["0.3", "1000"])
+def test_grouped_adamw_launches_match_per_bucket(monkeypatch, mparams):
+    """TH_OPT_GROUP_MPARAMS: AdamW over flat-contiguous bucket groups gives the per-bucket result
+    bit for bit, covers every owned element once and still completes every bucket."""
+    outs = {}
+    for group in ("0", mparams):
+        monkeypatch.setenv("TH_OPT_GROUP_MPARAMS", group)
+        m = _model()
+        store = FlatParamStore(m.params_in_backward_order(), torch.device("cpu"), bucket_mb=0.05)
+        opt = FlatAdamW(store, lr=1e-3, clip=0.0)
+        groups = opt._launch_groups()
+        runs = sorted(r for r, _ in groups if r is not None)
+        assert sum(b - a for a, b, _, _ in runs) == opt.local_numel  # every element exactly once
+        assert all(x[1] <= y[0] for x, y in zip(runs, runs[1:]))
+        assert sorted(bi for _, bs in groups for bi in bs) == list(range(len(opt.bucket_segments)))
+        if group == "0":
+            assert len(groups) == len(opt.segments)
+        else:
+            assert len(groups) < len(opt.segments)
+        data = SyntheticTokens(CFG.vocab_size, B, S, torch.device("cpu"), 0)
+        for _ in range(2):
+            _step_on(m, store, opt, [data.next()], B * S)
+        outs[group] = store.param_buf.clone()
+    assert torch.equal(outs["0"], outs[mparams])
