@@ -373,8 +373,9 @@ class FlatAdamW:
         if self.clip > 0:
             # ||g||^2 over maximal flat-contiguous runs (the sum does not care about decay groups)
             runs: list[tuple] = []
+            merge = os.environ.get("TH_OPT_SUMSQ_RUNS", "1") == "1"  # 0: one pass per segment (old form)
             for seg in self.segments:
-                m = self._merge(runs[-1], seg, same_wd=False) if runs else None
+                m = self._merge(runs[-1], seg, same_wd=False) if runs and merge else None
                 if m is not None and m[1] - m[0] <= (1 << 31) - 8:
                     runs[-1] = m
                 else:
