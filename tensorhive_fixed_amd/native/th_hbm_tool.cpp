@@ -21,9 +21,10 @@
 // instance; 4 TCC counters = one hardware pass).  TH_HBM_APPEND=1 appends lines instead
 // (calibration runs); TH_HBM_PERIOD_MS sets the period (default 1000).
 //
-// One counting session per GPU: a torchrun rank (LOCAL_RANK set) samples only the GPU it drives
-// (the LOCAL_RANK-th visible agent, as the payload binds cuda:LOCAL_RANK); TH_HBM_ALL_AGENTS=1
-// samples every visible GPU.
+// One counting session per GPU the task can use: HIP_VISIBLE_DEVICES (set by the daemon from the
+// reservation) limits the agents; a torchrun rank (LOCAL_RANK set) samples only the GPU it drives
+// (the LOCAL_RANK-th visible one, as the payload binds cuda:LOCAL_RANK); TH_HBM_ALL_AGENTS=1
+// samples every visible GPU (th_hbm_select.h).
 //
 // Validated on MI355X (profiles/r03_counters/): copy stream 4.79 TB/s counted vs 4.785 moved;
 // add stream 5.87 vs 5.76; the GEMM + SwiGLU mix 4.27 GB per iteration vs 4.04 from rocprofv3
@@ -42,12 +43,15 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <string>
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include "th_hbm_select.h"
 
 namespace {
 
@@ -123,13 +127,15 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
         return ROCPROFILER_STATUS_SUCCESS;
       },
       sizeof(rocprofiler_agent_v0_t), &agents);
-  const char* lr = getenv("LOCAL_RANK");
+  // HIP's physical order is the KFD node order; HIP_VISIBLE_DEVICES and LOCAL_RANK index into it
+  std::sort(agents.begin(), agents.end(),
+            [](const rocprofiler_agent_v0_t& x, const rocprofiler_agent_v0_t& y) { return x.node_id < y.node_id; });
   const char* all = getenv("TH_HBM_ALL_AGENTS");
-  if (lr && *lr && !(all && !strcmp(all, "1")) && !agents.empty()) {
-    const auto mine = agents[(size_t)atoi(lr) % agents.size()];
-    agents.assign(1, mine);
-  }
-  for (const auto& info : agents) {
+  std::vector<rocprofiler_agent_v0_t> chosen;
+  for (int i : th_hbm::select_agents((int)agents.size(), getenv("HIP_VISIBLE_DEVICES"), getenv("LOCAL_RANK"),
+                                     all && !strcmp(all, "1")))
+    chosen.push_back(agents[(size_t)i]);
+  for (const auto& info : chosen) {
     auto* a = new Agent();
     a->info = info;
     if (rocprofiler_create_context(&a->ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
