@@ -60,7 +60,7 @@ def test_custom_op_model_matches_reference_cpu():
     loss = model(tok, tgt)
     loss.backward()
     ref_loss, ref_grads = _reference_loss(model, tok, tgt)
-    assert abs(float(loss) - float(ref_loss)) < 2e-2
+    assert abs(float(loss.detach()) - float(ref_loss.detach())) < 2e-2
     for n, p in model.named_parameters():
         a, b = p.grad.float(), ref_grads[n]
         rel = float((a - b).norm() / (b.norm() + 1e-8))
@@ -103,7 +103,7 @@ def test_add_norm_flow_matches_addmm_epilogue_flow_cpu(monkeypatch):
         model = Llama(cfg, device="cpu", dtype=torch.bfloat16, seed=5)
         loss = model(tok, tgt)
         loss.backward()
-        out[flag] = (float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+        out[flag] = (float(loss.detach()), {n: p.grad.float().clone() for n, p in model.named_parameters()})
     assert abs(out[True][0] - out[False][0]) < 1e-2
     for n, a in out[True][1].items():
         b = out[False][1][n]
