@@ -7,6 +7,11 @@
 * Status semantics the web UI relies on: missing header -> 401, expired -> 401 (the SPA then
   refreshes and retries), revoked -> 401, malformed/wrong type -> 422, non-admin on an admin
   operation -> 403 ``{"msg": "Unprivileged"}``.
+* Tokens whose signature does not verify or that carry no ``exp`` are 401 (a key rotation then
+  sends the SPA through refresh -> login instead of showing an error).
+* No token is signed or accepted while ``[auth] secret_key`` is empty or a public default such
+  as the reference's ``jwt-some-secret`` (``tensorhive/config.py:289``), unless
+  ``TENSORHIVE_ALLOW_INSECURE_SECRET=1`` (tests only): anyone could forge an admin token.
 """
 from __future__ import annotations
 
@@ -14,8 +19,20 @@ from dataclasses import dataclass
 
 from flask import g, request
 
-from ..config import get_config
+from ..config import get_config, insecure_secret_allowed, secret_is_insecure
 from ..utils import jwt
+
+
+class InsecureSecret(RuntimeError):
+    """The configured signing key is empty or publicly known."""
+
+
+def signing_key() -> str:
+    key = get_config().auth.secret_key
+    if secret_is_insecure(key) and not insecure_secret_allowed():
+        raise InsecureSecret("[auth] secret_key is empty or a public default; run `tensorhive init` "
+                             "or set a random secret_key in main_config.ini")
+    return key
 
 
 class AuthError(Exception):
@@ -44,17 +61,17 @@ def _responses():
 
 def create_access_token(user_id: int, roles: list[str], fresh: bool = False) -> str:
     a = get_config().auth
-    return jwt.create_token(user_id, "access", a.secret_key, a.access_token_expires, fresh=fresh,
+    return jwt.create_token(user_id, "access", signing_key(), a.access_token_expires, fresh=fresh,
                             user_claims={"roles": list(roles)})
 
 
 def create_refresh_token(user_id: int) -> str:
     a = get_config().auth
-    return jwt.create_token(user_id, "refresh", a.secret_key, a.refresh_token_expires)
+    return jwt.create_token(user_id, "refresh", signing_key(), a.refresh_token_expires)
 
 
 def decode_token(token: str) -> dict:
-    return jwt.decode(token, get_config().auth.secret_key)
+    return jwt.decode(token, signing_key())
 
 
 def _bearer() -> str:
@@ -76,6 +93,10 @@ def verify(required_type: str = "access") -> Identity:
         claims = decode_token(_bearer())
     except jwt.ExpiredSignature:
         raise AuthError(401, _responses()["token"]["expired"])
+    except (jwt.InvalidSignature, jwt.MissingClaim) as e:
+        raise AuthError(401, str(e))
+    except InsecureSecret as e:
+        raise AuthError(401, str(e))
     except jwt.JWTError as e:
         raise AuthError(422, str(e))
     ttype = claims.get("type")

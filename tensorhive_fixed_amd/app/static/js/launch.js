@@ -6,10 +6,11 @@
 
 // One shell word per value, as the server renders it (models/orm.py _shell_value): a value the
 // shell already reads as one word stays as typed (the user's own quoting, globs, $VARS); values
-// that would split, have an unbalanced quote or an unquoted operator, and JSON documents
+// that would split, have an unbalanced quote, an unquoted operator, a leading # (comment) or a
+// brace expansion ({a,b}, {1..3}), and JSON documents
 // (TF_CONFIG), are single-quoted.  isOneShellWord mirrors _is_one_shell_word line for line.
 export function isOneShellWord(v) {
-  let words = 0, inWord = false, quote = "", i = 0;
+  let words = 0, inWord = false, quote = "", brace = 0, i = 0;
   while (i < v.length) {
     const c = v[i];
     if (quote === "'") {
@@ -18,13 +19,22 @@ export function isOneShellWord(v) {
       if (c === "\\") i += 1;
       else if (c === '"') quote = "";
     } else if (" \t\n".includes(c)) {
-      inWord = false;
+      inWord = false; brace = 0;
     } else if (";&|<>()".includes(c)) {
       return false;
     } else {
-      if (!inWord) { words += 1; inWord = true; }
+      if (!inWord) {
+        if (c === "#") return false;
+        words += 1; inWord = true;
+      }
       if (c === "\\") i += 1;
       else if (c === "'" || c === '"') quote = c;
+      else if (c === "{") brace = 1;
+      else if (brace && (c === "," || (c === "." && v.slice(i + 1, i + 2) === "."))) brace = 2;
+      else if (c === "}") {
+        if (brace === 2) return false;
+        brace = 0;
+      }
     }
     i += 1;
   }

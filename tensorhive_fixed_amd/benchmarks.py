@@ -77,6 +77,7 @@ probe_enabled = off
 log_dir = {d / 'logs'}
 """)
         C.init_config_files(d)
+        C.ensure_secret_key(d / "main_config.ini")
         os.environ["TENSORHIVE_CONFIG_DIR"] = str(d)
         os.environ["TH_RUN_STATE_DIR"] = str(d / "th-run")
         cfg = C.load_config(d)

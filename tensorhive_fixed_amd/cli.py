@@ -72,7 +72,7 @@ def do_init() -> None:
     """3-step wizard: public hostname -> DB -> first account (reference ``cli.py:169-214``)."""
     import configparser
 
-    from .config import config_dir, get_config, load_config, set_config
+    from .config import config_dir, ensure_secret_key, get_config, load_config, set_config
     from .core.account_creator import AccountCreator
     from .database import configure, ensure_db_with_current_schema
 
@@ -86,6 +86,9 @@ def do_init() -> None:
     cp.set("api", "url_hostname", host)
     with open(path, "w") as f:
         cp.write(f)
+    os.chmod(path, 0o600)
+    if ensure_secret_key(path):  # an install upgraded from the reference still has its public key
+        click.echo("wrote a new random [auth] secret_key")
     set_config(load_config())
     click.echo("[2/3] database")
     configure()
@@ -119,6 +122,21 @@ def main(ctx, version, log_level, log_dir, config_dir, json_logs):
     run_daemon()
 
 
+def refuse_insecure_secret(cfg) -> None:
+    """Exit when the JWT signing key is empty or public (anyone reaching :1111 could mint an admin
+    token and run jobs as any user); ``TENSORHIVE_ALLOW_INSECURE_SECRET=1`` overrides (tests)."""
+    from .config import ALLOW_INSECURE_ENV, insecure_secret_allowed, secret_is_insecure
+
+    if not secret_is_insecure(cfg.auth.secret_key):
+        return
+    if insecure_secret_allowed():
+        logging.getLogger(__name__).warning("[auth] secret_key is public; allowed by %s", ALLOW_INSECURE_ENV)
+        return
+    raise click.ClickException(
+        f"[auth] secret_key in {cfg.directory / 'main_config.ini'} is empty or the public default "
+        "'jwt-some-secret'; run `tensorhive init` (writes a random key) or set one yourself")
+
+
 def run_daemon(block: bool = True):
     from .api.app import create_app
     from .app.server import AppServer, serve_wsgi
@@ -127,6 +145,7 @@ def run_daemon(block: bool = True):
     from .database import check_if_db_exists, configure, ensure_db_with_current_schema
 
     cfg = get_config()
+    refuse_insecure_secret(cfg)
     if not check_if_db_exists():
         do_init()
     configure()

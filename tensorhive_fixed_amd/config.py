@@ -20,6 +20,8 @@ import ast
 import configparser
 import logging
 import os
+import re
+import secrets
 import shutil
 import threading
 from dataclasses import dataclass, field
@@ -40,9 +42,63 @@ def config_dir() -> Path:
     return Path(os.environ.get("TENSORHIVE_CONFIG_DIR", str(DEFAULT_CONFIG_DIR))).expanduser()
 
 
+# signing keys that are public knowledge: the reference ships ``jwt-some-secret`` in its template
+# and as the fallback (``tensorhive/config.py:289``, ``main_config.ini:75``), so with it anyone who
+# reaches the API can mint an admin token
+INSECURE_SECRETS = frozenset({"", "jwt-some-secret", "secret", "changeme"})
+ALLOW_INSECURE_ENV = "TENSORHIVE_ALLOW_INSECURE_SECRET"
+_SECRET_LINE = re.compile(r"^(\s*secret_key\s*=)[ \t]*(.*)$", re.M)
+
+
+def secret_is_insecure(secret: str | None) -> bool:
+    return (secret or "").strip() in INSECURE_SECRETS
+
+
+def insecure_secret_allowed() -> bool:
+    return os.environ.get(ALLOW_INSECURE_ENV, "") in ("1", "yes", "true")
+
+
+def new_secret() -> str:
+    return secrets.token_hex(32)  # 256 bits
+
+
+def ensure_secret_key(path: Path | str) -> bool:
+    """Give ``main_config.ini`` a random ``[auth] secret_key`` when it has none or the public
+    default (keeps the file's other lines and its 0600 mode). Returns True when it wrote one."""
+    p = Path(path).expanduser()
+    try:
+        text = p.read_text()
+    except OSError:
+        return False
+    cp = configparser.ConfigParser(strict=False)
+    cp.read_string(text)
+    current = None
+    for k in ("secret_key", "secrect_key"):
+        if cp.has_option("auth", k):
+            current = cp.get("auth", k)
+            break
+    if current is not None and not secret_is_insecure(current):
+        return False
+    key = new_secret()
+    if current is not None and _SECRET_LINE.search(text):
+        text = _SECRET_LINE.sub(lambda m: f"{m.group(1)} {key}", text, count=1)
+    elif re.search(r"^\[auth\]\s*$", text, re.M):
+        text = re.sub(r"^\[auth\]\s*$", f"[auth]\nsecret_key = {key}", text, count=1, flags=re.M)
+    else:
+        text = text.rstrip("\n") + f"\n\n[auth]\nsecret_key = {key}\n"
+    tmp = p.with_name(p.name + ".tmp")
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    with os.fdopen(fd, "w") as f:
+        f.write(text)
+    os.replace(tmp, p)
+    log.warning("wrote a new random [auth] secret_key to %s (tokens signed with the old key are void)", p)
+    return True
+
+
 def init_config_files(directory: Path | None = None) -> list[Path]:
     """Copy missing INI templates into ``directory`` (mode 0600); never overwrite. Returns the
-    list of files created (reference: ``ConfigInitilizer``, ``config.py:31-69``)."""
+    list of files created (reference: ``ConfigInitilizer``, ``config.py:31-69``). A freshly
+    created ``main_config.ini`` gets a random 256-bit ``[auth] secret_key``."""
     d = Path(directory or config_dir()).expanduser()
     d.mkdir(parents=True, exist_ok=True)
     created = []
@@ -52,6 +108,8 @@ def init_config_files(directory: Path | None = None) -> list[Path]:
             continue
         shutil.copy(TEMPLATE_DIR / name, dst)
         os.chmod(dst, 0o600)
+        if name == "main_config.ini":
+            ensure_secret_key(dst)
         created.append(dst)
         log.info("created %s", dst)
     return created
@@ -255,6 +313,9 @@ class LauncherConfig:
     rccl_max_nchannels: str = ""
     rccl_algo: str = ""
     rccl_proto: str = ""
+    # node-local path of libthhbm.so on REMOTE nodes (empty = remote tasks are not counted); the
+    # daemon's own node always uses this install's copy
+    hbm_tool: str = ""
 
 
 @dataclass
@@ -316,7 +377,7 @@ def load_config(directory: Path | str | None = None) -> Config:
     nodes, proxy = parse_hosts(hosts_file)
     db_path = str(Path(main.str("database", "path", str(d / "database.sqlite"))).expanduser())
     db_uri = "sqlite://" if os.environ.get("PYTEST") else f"sqlite:///{db_path}"
-    secret = main.str("auth", ("secret_key", "secrect_key"), "jwt-some-secret")
+    secret = main.str("auth", ("secret_key", "secrect_key"), "")
     tmpl = _Reader(load_ini(TEMPLATE_DIR / "mailbot_config.ini", "mailbot-template"))
     jobs_sections = ("job_scheduling_service", "task_scheduling_service")
     return Config(
@@ -424,6 +485,7 @@ def load_config(directory: Path | str | None = None) -> Config:
             rccl_max_nchannels=main.str("launcher", "rccl_max_nchannels", ""),
             rccl_algo=main.str("launcher", "rccl_algo", ""),
             rccl_proto=main.str("launcher", "rccl_proto", ""),
+            hbm_tool=main.str("launcher", "hbm_tool", ""),
         ),
     )
 

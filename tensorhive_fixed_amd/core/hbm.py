@@ -8,16 +8,21 @@ do this -- on this stack the TCC request counters only count the counting proces
 (``profiles/r03_counters/``) -- so the task counts itself and the monitor sums the files per GPU.
 
 :func:`read_rates` returns ``{bdf: {"hbm_read": GB/s, "hbm_write": GB/s, "pids": [...]}}`` over
-the live, fresh files; files of dead processes are removed.  GPUs without a counting task keep
-libthsmi's ``mem_activity_acc``-based ``hbm_bw`` estimate (``hbm_bw_source`` says which).
+the live, fresh files whose owner owns the pid; files of dead processes are removed.
+:func:`metrics_for` keeps only pids libthsmi lists on that GPU as th-run task processes.  GPUs
+without a counting task keep libthsmi's ``mem_activity_acc``-based ``hbm_bw`` estimate; GPUs
+where only some processes are counted say ``partial`` (``hbm_bw_source`` says which).
 """
 from __future__ import annotations
 
 import glob
 import json
+import logging
 import os
 import time
 from pathlib import Path
+
+log = logging.getLogger(__name__)
 
 SHM_GLOB = "/dev/shm/th-hbm-*.json"
 
@@ -45,44 +50,106 @@ def _alive(pid: int) -> bool:
         return True
 
 
+def _proc_uid(pid: int) -> int | None:
+    try:
+        return os.stat(f"/proc/{pid}").st_uid
+    except OSError:
+        return None
+
+
 def read_rates(pattern: str = SHM_GLOB, max_age_s: float = 5.0, now: float | None = None,
                cleanup: bool = True) -> dict[str, dict]:
+    """``{bdf: {"hbm_read", "hbm_write", "pids", "by_pid": {pid: (rd GB/s, wr GB/s)}}}`` over the
+    fresh files of live processes. A file is taken only when its owner is the owner of the pid it
+    names (``/dev/shm`` is world-writable: anyone could otherwise write a file naming pid 1 or a
+    victim's training process); :func:`metrics_for` then checks the pid against the GPU's own
+    process list."""
     now = time.time() if now is None else now
     out: dict[str, dict] = {}
     for f in glob.glob(pattern):
         try:
+            st = os.stat(f)
             doc = json.loads(Path(f).read_text())
-        except (OSError, ValueError):
+            pid = int(doc.get("pid") or 0)
+        except (OSError, ValueError, TypeError):
             continue
-        pid = int(doc.get("pid") or 0)
-        if pid and not _alive(pid):
+        if pid <= 0:
+            continue
+        if not _alive(pid):
             if cleanup:
                 try:
                     os.unlink(f)
                 except OSError:
                     pass
             continue
+        if _proc_uid(pid) != st.st_uid:
+            log.warning("hbm: ignoring %s: file owner uid %d is not the owner of pid %d", f, st.st_uid, pid)
+            continue
         if now - int(doc.get("ts_ns", 0)) / 1e9 > max_age_s:
             continue
         win = max(float(doc.get("window_ms") or 0.0), 1e-3) / 1000.0
         for g in doc.get("gpus", []):
-            r = out.setdefault(g.get("bdf"), {"hbm_read": 0.0, "hbm_write": 0.0, "pids": []})
-            r["hbm_read"] += float(g.get("rd_bytes") or 0.0) / win / 1e9
-            r["hbm_write"] += float(g.get("wr_bytes") or 0.0) / win / 1e9
+            rd = float(g.get("rd_bytes") or 0.0) / win / 1e9
+            wr = float(g.get("wr_bytes") or 0.0) / win / 1e9
+            r = out.setdefault(g.get("bdf"), {"hbm_read": 0.0, "hbm_write": 0.0, "pids": [], "by_pid": {}})
+            r["hbm_read"] += rd
+            r["hbm_write"] += wr
             r["pids"].append(pid)
+            prd, pwr = r["by_pid"].get(pid, (0.0, 0.0))
+            r["by_pid"][pid] = (prd + rd, pwr + wr)
     return out
 
 
 def metrics_for(gpus: list[dict], rates: dict[str, dict]) -> dict[int, dict]:
-    """``{index: metrics}`` for the GPUs that have counted traffic: hbm_read / hbm_write and an
-    ``hbm_bw`` that replaces the activity-based estimate, with ``hbm_bw_source = counters``."""
+    """``{index: metrics}`` for the GPUs with counted traffic.
+
+    A counted pid is kept only if libthsmi lists it on that very GPU with a ``TENSORHIVE_TASK_ID``
+    (a th-run task's process); any other file is ignored and logged.  Then:
+
+    * every process on the GPU is counted -> ``hbm_bw`` = counted read + write,
+      ``hbm_bw_source = counters``;
+    * some process on the GPU is not counted (a foreign tenant, a task without the tool) ->
+      ``hbm_bw_source = partial``: ``hbm_bw`` keeps the device-wide activity estimate (raised to
+      the counted sum if that is larger), ``hbm_counted`` carries the counted part.  An uncounted
+      tenant never reads as 0 GB/s behind a ``counters`` label.
+
+    GPU records without a ``processes`` key (callers that have no process list) keep the old
+    behaviour: every file that names the GPU counts."""
     out = {}
     for g in gpus:
         r = rates.get(g.get("bdf"))
         if r is None:
             continue
-        rd, wr = round(r["hbm_read"], 1), round(r["hbm_write"], 1)
-        out[g["index"]] = {"hbm_read": {"value": rd, "unit": "GB/s"}, "hbm_write": {"value": wr, "unit": "GB/s"},
-                           "hbm_bw": {"value": round(rd + wr, 1), "unit": "GB/s"},
-                           "hbm_bw_source": {"value": "counters", "unit": ""}}
+        procs = g.get("processes")
+        by_pid = r.get("by_pid") or {p: (r["hbm_read"] / max(1, len(r["pids"])),
+                                         r["hbm_write"] / max(1, len(r["pids"]))) for p in r.get("pids", [])}
+        if procs is None:
+            valid = dict(by_pid)
+            uncounted = []
+        else:
+            tasks = {int(p["pid"]): p.get("task_id") for p in procs if p.get("pid") is not None}
+            valid = {}
+            for pid, v in by_pid.items():
+                if pid in tasks and tasks[pid] not in (None, ""):
+                    valid[pid] = v
+                else:
+                    log.warning("hbm: ignoring counts of pid %d on %s: %s", pid, g.get("bdf"),
+                                "not a th-run task process" if pid in tasks else "not a process of this GPU")
+            uncounted = [p for p in tasks if p not in valid]
+        if not valid:
+            continue
+        rd = round(sum(v[0] for v in valid.values()), 1)
+        wr = round(sum(v[1] for v in valid.values()), 1)
+        m = {"hbm_read": {"value": rd, "unit": "GB/s"}, "hbm_write": {"value": wr, "unit": "GB/s"},
+             "hbm_counted": {"value": round(rd + wr, 1), "unit": "GB/s"}}
+        if uncounted:
+            est = ((g.get("metrics") or {}).get("hbm_bw") or {}).get("value")
+            total = max(float(est or 0.0), rd + wr)
+            m["hbm_bw"] = {"value": round(total, 1), "unit": "GB/s"}
+            m["hbm_bw_source"] = {"value": "partial", "unit": ""}
+            m["hbm_uncounted_pids"] = {"value": len(uncounted), "unit": ""}
+        else:
+            m["hbm_bw"] = {"value": round(rd + wr, 1), "unit": "GB/s"}
+            m["hbm_bw_source"] = {"value": "counters", "unit": ""}
+        out[g["index"]] = m
     return out

@@ -94,22 +94,49 @@ def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | No
     return f"if command -v {th} >/dev/null 2>&1 || [ -x {th} ]; then {primary}; else {fallback}; fi"
 
 
-def spawn_env(hostname: str) -> dict[str, str]:
-    """Environment th-run gives every task on ``hostname`` besides ``TENSORHIVE_TASK_ID``: on the
-    daemon's own node, the in-task HBM counter tool (``[amd_monitor] task_hbm_counters``,
-    ``core/hbm.py``), whose per-process files only the local monitor reads."""
+# profilers that open their own counter sessions: a task running one must not also carry the
+# in-task counter tool (one device-counting session per GPU; the profiler's would lose)
+_PROFILERS = ("rocprofv3", "rocprofv2", "rocprof", "rocprof-compute", "rocprof-sys-run", "omniperf")
+
+
+def runs_profiler(command: str) -> bool:
+    """Whether ``command`` runs a rocprofiler-based profiler, or opts out of the counter tool with
+    ``TENSORHIVE_HBM_COUNTERS=0``."""
+    try:
+        words = shlex.split(command)
+    except ValueError:
+        words = command.split()
+    for w in words:
+        if w in ("TENSORHIVE_HBM_COUNTERS=0", "TENSORHIVE_HBM_COUNTERS=no"):
+            return True
+        if w.rsplit("/", 1)[-1] in _PROFILERS:
+            return True
+    return False
+
+
+def spawn_env(hostname: str, command: str = "") -> dict[str, str]:
+    """Environment th-run gives every task on ``hostname`` besides ``TENSORHIVE_TASK_ID``: the
+    in-task HBM counter tool (``[amd_monitor] task_hbm_counters``, ``core/hbm.py``) -- this
+    install's ``libthhbm`` on the daemon's own node, ``[launcher] hbm_tool`` (a path on the node)
+    on remote nodes, whose node agent publishes the files (``agent.py``).  Left out when the
+    command runs a profiler (``tensorhive profile --pmc``) or says ``TENSORHIVE_HBM_COUNTERS=0``."""
     cfg = get_config()
+    if not getattr(cfg.amd_monitor, "task_hbm_counters", False) or runs_profiler(command):
+        return {}
     spec = cfg.ssh.available_nodes.get(hostname, {})
-    if spec.get("transport") == "local" and getattr(cfg.amd_monitor, "task_hbm_counters", False):
+    if spec.get("transport") == "local":
         from .hbm import task_env
 
         return task_env()
+    remote_tool = getattr(cfg.launcher, "hbm_tool", "")
+    if remote_tool and spec.get("transport", "ssh") == "ssh":
+        return {"ROCP_TOOL_LIBRARIES": remote_tool}
     return {}
 
 
 def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra_env: dict | None = None,
           max_restarts: int = 0) -> int:
-    env = {**spawn_env(hostname), **(extra_env or {})}
+    env = {**spawn_env(hostname, command), **(extra_env or {})}
     r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), env,
                                                  max_restarts))
     if r.exception is not None:

@@ -53,9 +53,10 @@ def _utcnow():
 
 
 def _is_one_shell_word(v: str) -> bool:
-    """Would ``bash`` read ``v`` as exactly one word with no unquoted control operator?
+    """Would ``bash`` read ``v`` as exactly one word with no unquoted control operator, no
+    comment (a word starting with ``#``) and no brace expansion (``{a,b}``, ``{1..3}``)?
     (A small scanner, mirrored line for line by ``app/static/js/launch.js``.)"""
-    words, in_word, quote, i = 0, False, "", 0
+    words, in_word, quote, brace, i = 0, False, "", 0, 0
     while i < len(v):
         c = v[i]
         if quote == "'":
@@ -67,16 +68,26 @@ def _is_one_shell_word(v: str) -> bool:
             elif c == '"':
                 quote = ""
         elif c in " \t\n":
-            in_word = False
+            in_word, brace = False, 0
         elif c in ";&|<>()":
             return False
         else:
             if not in_word:
+                if c == "#":
+                    return False
                 words, in_word = words + 1, True
             if c == "\\":
                 i += 1
             elif c in "'\"":
                 quote = c
+            elif c == "{":
+                brace = 1
+            elif brace and (c == "," or (c == "." and v[i + 1:i + 2] == ".")):
+                brace = 2
+            elif c == "}":
+                if brace == 2:
+                    return False
+                brace = 0
         i += 1
     return words == 1 and quote == "" and i == len(v)
 

@@ -165,7 +165,11 @@ class _QKVAttention(torch.autograd.Function):
         B, S, Hq, Hkv, Dh, theta = ctx.dims
         if ctx.backend == "hip" and do.is_cuda:
             qkv, o, lse = ctx.saved_tensors
-            if _ROPE_FUSED and _BWD_FLAGS == 0 and Dh == 128:  # rotary backward inside the kernels
+            # rotary backward inside the kernels; the fused path needs 32-bit LDS-DMA offsets
+            # (S * row * 2 B < 2^31, flash_attn.hip flash_bwd_impl), longer rows take the
+            # register-staged kernels + a separate rotary pass
+            row = qkv.shape[1]
+            if _ROPE_FUSED and _BWD_FLAGS == 0 and Dh == 128 and S * row * 2 < (1 << 31):
                 tabs = rope_tables(S, Dh, theta, do.device)
                 return (flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh, flags=_BWD_FLAGS, rope=tabs),
                         None, None, None, None, None, None, None)

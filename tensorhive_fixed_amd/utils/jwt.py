@@ -23,6 +23,14 @@ class ExpiredSignature(JWTError):
     pass
 
 
+class InvalidSignature(JWTError):
+    pass
+
+
+class MissingClaim(JWTError):
+    pass
+
+
 def _b64(b: bytes) -> str:
     return base64.urlsafe_b64encode(b).decode("ascii").rstrip("=")
 
@@ -40,6 +48,8 @@ def encode(payload: dict, secret: str) -> str:
 
 
 def decode(token: str, secret: str, leeway: float = 0.0, now: float | None = None) -> dict:
+    """Verify and return the claims. A bad signature raises :class:`InvalidSignature`, a token
+    without a numeric ``exp`` :class:`MissingClaim`, an expired one :class:`ExpiredSignature`."""
     try:
         h, p, s = token.split(".")
         header = json.loads(_unb64(h))
@@ -51,9 +61,13 @@ def decode(token: str, secret: str, leeway: float = 0.0, now: float | None = Non
         raise JWTError("unsupported algorithm")
     want = hmac.new(secret.encode(), f"{h}.{p}".encode(), hashlib.sha256).digest()
     if not hmac.compare_digest(sig, want):
-        raise JWTError("signature verification failed")
+        raise InvalidSignature("signature verification failed")
     t = time.time() if now is None else now
-    if "exp" in payload and t > payload["exp"] + leeway:
+    # every token this server issues expires; one without ``exp`` was minted elsewhere and would
+    # otherwise be valid forever
+    if not isinstance(payload.get("exp"), (int, float)):
+        raise MissingClaim("token has no expiry")
+    if t > payload["exp"] + leeway:
         raise ExpiredSignature("token has expired")
     if "nbf" in payload and t + leeway < payload["nbf"]:
         raise JWTError("token not yet valid")

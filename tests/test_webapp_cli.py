@@ -356,7 +356,8 @@ def test_scaling_bucket_sweep_records_each_size_and_the_best():
 
 SHELL_CASES = ['"a b"', "/data/*.tfrecord", "$HOME/x", "~/ckpt", "a b", "a;b", '"a;b"', "it's", "--x=1",
                '{"a": 1}', '{"cluster":{"w":["h:1"]}}', "a\\ b", "x\\", "'quoted already'", "a&&b", "(x)",
-               "tcp://127.0.0.1:29500", "", "{a,b}", 'say "hi there"']
+               "tcp://127.0.0.1:29500", "", "{a,b}", 'say "hi there"', "#1", "a#b", "x{1..3}",
+               "{a}", "${HOME}", "--tag=#x"]
 
 
 def test_shell_value_keeps_one_word_values_and_js_agrees(tmp_path):
@@ -369,12 +370,22 @@ def test_shell_value_keeps_one_word_values_and_js_agrees(tmp_path):
 
     expect = {'"a b"': '"a b"', "/data/*.tfrecord": "/data/*.tfrecord", "$HOME/x": "$HOME/x", "a b": "'a b'",
               "a;b": "'a;b'", '"a;b"': '"a;b"', "it's": "'it'\\''s'", '{"a": 1}': "'{\"a\": 1}'",
-              "'quoted already'": "'quoted already'", "x\\": "'x\\'", "": ""}
+              "'quoted already'": "'quoted already'", "x\\": "'x\\'", "": "",
+              # a leading # would comment out the rest of the command, a brace list
+              # would expand into several words (shlex does neither, so check the rendering)
+              "#1": "'#1'", "a#b": "a#b", "{a,b}": "'{a,b}'", "x{1..3}": "'x{1..3}'", "{a}": "{a}",
+              "${HOME}": "${HOME}"}
     for v, want in expect.items():
         assert _shell_value(v) == want, v
     for v in SHELL_CASES:  # every rendered value is exactly one shell word
         if v:
             assert len(_shlex.split(_shell_value(v))) == 1, v
+    # ... and bash agrees (brace expansion and comments are bash's, not shlex's)
+    import subprocess as _sp
+
+    script = "\n".join(f"set -- {_shell_value(v)} END; echo $#" for v in SHELL_CASES if v)
+    counts = _sp.run(["bash", "--norc", "-c", script], capture_output=True, text=True, cwd=tmp_path).stdout.split()
+    assert counts == ["2"] * len([v for v in SHELL_CASES if v]), list(zip(SHELL_CASES, counts))
     out = _node_eval(tmp_path, r"""
 import { shellValue } from "@JS@/launch.js";
 console.log(JSON.stringify(%s.map(shellValue)));
