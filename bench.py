@@ -65,11 +65,16 @@ def main() -> int:
                     help="rank 0 also measures the daemon's dashboard poll latency after the timed steps")
     args = ap.parse_args()
 
+    from tensorhive_fixed_amd.utils.blas_env import refuse_unsafe_blas_workspace
+
+    refuse_unsafe_blas_workspace("bench")  # a known hipBLASLt fault; nothing touched the GPU yet
+
     import torch
 
     from tensorhive_fixed_amd.models.llama3 import LlamaConfig
     from tensorhive_fixed_amd.ops import _lib
     from tensorhive_fixed_amd.ops.attention import attention_backend
+    from tensorhive_fixed_amd.parallel.comm_diag import comm_report
     from tensorhive_fixed_amd.parallel.dist import barrier, init_distributed, rank_census, shutdown
     from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer, run_timed
 
@@ -83,6 +88,7 @@ def main() -> int:
                  zero=args.zero)
     res = run_timed(tr, args.steps, args.warmup)
     census = rank_census(info)  # collective: every rank takes part, after the timed region
+    comm = comm_report(res["waits"], info)  # collective too: per-rank exposed-communication spans
     n = info.world
     flops = cfg.flops_per_token(args.seq_len) * res["tokens_per_sec"]
     line = {
@@ -115,7 +121,12 @@ def main() -> int:
         "tflops_per_gpu": round(flops / n / 1e12, 1),
         "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
         "final_loss": round(res["loss"], 4),
-        "dist": census,
+        # where a step's time went besides compute (max over ranks, ms per step): the compute stream's
+        # stalls on gradient buckets + parameter all-gathers, and on the overlapped optimizer
+        "exposed_comm_ms_per_step": comm["exposed_comm_ms_per_step"],
+        "allgather_wait_ms": comm["allgather_wait_ms"],
+        "opt_wait_ms": comm["opt_wait_ms"],
+        "dist": {**census, "comm": comm},
     }
     if info.is_main:
         line["daemon"] = daemon_poll_latency() if args.daemon_bench else None

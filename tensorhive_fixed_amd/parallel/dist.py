@@ -87,6 +87,10 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = os.environ.get("TH_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
         kw = {"device_id": device} if backend == "nccl" else {}
+        if backend == "nccl":  # RCCL's init log -> a per-rank file bench.py summarises (comm_diag.py)
+            from .comm_diag import prepare_rccl_log
+
+            prepare_rccl_log(rank)
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     elif dist.is_initialized():
         backend = dist.get_backend()

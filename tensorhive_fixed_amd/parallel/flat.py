@@ -42,6 +42,9 @@ from __future__ import annotations
 
 import math
 import os
+import time
+from collections import defaultdict
+from contextlib import contextmanager
 from dataclasses import dataclass, field
 
 import torch
@@ -55,6 +58,57 @@ _ALIGN = 64  # elements; keeps every view 128-byte aligned and every range a mul
 
 def _round_up(n: int, a: int) -> int:
     return (n + a - 1) // a * a
+
+
+class WaitTimer:
+    """Exposed-communication accounting: how long the compute stream stalls at each wait.
+
+    A wait on an async collective (``work.wait()`` on RCCL) or on the side-stream optimizer makes
+    the *current stream* wait; an event recorded just before and one just after the wait bound
+    that stall on the device timeline, so ``elapsed(before, after)`` is exactly the part of the
+    collective that was NOT hidden behind compute.  With gloo (CPU) the wait blocks the host and
+    the span is host time.  Categories: ``grad_sync`` (gradient buckets at the end of backward),
+    ``allgather`` (sharded parameters the next forward needs), ``opt_wait`` (the overlapped AdamW
+    the next backward / forward layer waits for).  Event pairs are resolved lazily by
+    :meth:`totals_ms` (one synchronize), so timing adds no host sync to a step."""
+
+    CATEGORIES = ("grad_sync", "allgather", "opt_wait")
+
+    def __init__(self, device: torch.device, enabled: bool = True):
+        self.cuda = torch.device(device).type == "cuda"
+        self.enabled = enabled
+        self.reset()
+
+    def reset(self) -> None:
+        self._events: list[tuple[str, object, object]] = []
+        self._host: dict[str, float] = defaultdict(float)
+        self.counts: dict[str, int] = defaultdict(int)
+
+    @contextmanager
+    def span(self, cat: str):
+        if not self.enabled:
+            yield
+            return
+        if self.cuda:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            yield
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._events.append((cat, e0, e1))
+        else:
+            t0 = time.perf_counter()
+            yield
+            self._host[cat] += time.perf_counter() - t0
+        self.counts[cat] += 1
+
+    def totals_ms(self) -> dict[str, float]:
+        out = {c: 1000.0 * self._host.get(c, 0.0) for c in self.CATEGORIES}
+        if self._events:
+            self._events[-1][2].synchronize()
+            for cat, e0, e1 in self._events:
+                out[cat] = out.get(cat, 0.0) + float(e0.elapsed_time(e1))
+        return out
 
 
 @dataclass
@@ -123,6 +177,8 @@ class FlatParamStore:
         self.accumulating = False
         self._sync_now = True
         self._ready_seen: set[int] = set()
+        # exposed-communication spans (bench.py reports them per rank); TH_COMM_TIMING=0 disables
+        self.timer = WaitTimer(self.device, enabled=os.environ.get("TH_COMM_TIMING", "1") == "1")
 
     # ------------------------------------------------------------------ buckets
     def _layout(self, entries: list, bucket_mb: float) -> tuple[list[int], list[_Bucket]]:
@@ -195,9 +251,10 @@ class FlatParamStore:
         for b in self.buckets:
             if b.handle is None:
                 b.handle = self._launch_grad_collective(b)
-        for b in self.buckets:
-            b.handle.wait()
-            b.handle = None
+        with self.timer.span("grad_sync"):
+            for b in self.buckets:
+                b.handle.wait()
+                b.handle = None
 
     # ------------------------------------------------------------------ sharded (ZeRO-1) helpers
     def owned_ranges(self) -> list[tuple[int, int]]:
@@ -232,23 +289,22 @@ class FlatParamStore:
         all-gather (sharded) or their overlapped optimizer update."""
         for p in params:
             b = self.param_bucket.get(id(p))
-            if b is None:
-                continue
-            if b.gather is not None:
+            if b is not None:
+                self._wait_bucket(b)
+
+    def _wait_bucket(self, b: _Bucket) -> None:
+        if b.gather is not None:
+            with self.timer.span("allgather"):
                 b.gather.wait()
-                b.gather = None
-            if b.updated is not None:
+            b.gather = None
+        if b.updated is not None:
+            with self.timer.span("opt_wait"):
                 torch.cuda.current_stream(self.device).wait_event(b.updated)
-                b.updated = None
+            b.updated = None
 
     def wait_all_params(self) -> None:
         for b in self.buckets:
-            if b.gather is not None:
-                b.gather.wait()
-                b.gather = None
-            if b.updated is not None:
-                torch.cuda.current_stream(self.device).wait_event(b.updated)
-                b.updated = None
+            self._wait_bucket(b)
 
 
 class FlatAdamW:
@@ -318,7 +374,8 @@ class FlatAdamW:
     def wait_done(self) -> None:
         """Current stream waits for the whole (overlapped) optimizer step."""
         if self.done is not None:
-            torch.cuda.current_stream(self.store.device).wait_event(self.done)
+            with self.store.timer.span("opt_wait"):
+                torch.cuda.current_stream(self.store.device).wait_event(self.done)
             self.done = None
 
     @staticmethod

@@ -179,17 +179,21 @@ def run_timed(trainer: Trainer, steps: int, warmup: int) -> dict:
     sync_device(info)
     barrier(info)
     sync_device(info)
+    trainer.store.timer.reset()  # exposed-communication spans of the timed steps only
     t0 = time.perf_counter()
     for _ in range(steps):
         trainer.step()
     sync_device(info)
     barrier(info)
     sync_device(info)
-    dt = max_over_ranks(time.perf_counter() - t0, info)
+    mine = time.perf_counter() - t0
+    dt = max_over_ranks(mine, info)
     loss = float(trainer.last_loss) if trainer.last_loss is not None else float("nan")
     toks = trainer.tokens_per_step * info.world * steps
+    waits = {f"{k}_ms_per_step": round(v / max(1, steps), 3) for k, v in trainer.store.timer.totals_ms().items()}
+    waits["step_ms"] = round(1000.0 * mine / max(1, steps), 3)
     return {"seconds": dt, "ms_per_step": 1000.0 * dt / max(1, steps), "tokens_per_sec": toks / dt,
-            "loss": loss}
+            "loss": loss, "waits": waits}
 
 
 def _maybe_save(tr: Trainer, ckpt: str | None, args) -> None:
@@ -213,6 +217,9 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--ckpt-every", type=int, default=0)
     ap.add_argument("--resume", action="store_true", help="continue from <ckpt-dir>/ckpt.pt if present")
     args = ap.parse_args(argv)
+    from ..utils.blas_env import refuse_unsafe_blas_workspace
+
+    refuse_unsafe_blas_workspace("th-train")
     info = init_distributed()
     cfg = LlamaConfig.named(args.model)
     tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb,
