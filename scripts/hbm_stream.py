@@ -3,8 +3,10 @@
 KIND ``add`` runs ``y += x`` over 1 GiB fp32 tensors (a shader kernel: 2 reads + 1 write per
 element), ``copy`` runs ``y.copy_(x)`` (the runtime's blit kernel).  Prints one JSON line with
 the bytes moved and the rate torch measured, so a counter sampler running beside it can be
-checked against a number that does not come from counters."""
+checked against a number that does not come from counters.  ``HBM_STREAM_START_AT`` (unix
+seconds) delays the start, so concurrent streams cover the same window."""
 import json
+import os
 import sys
 import time
 
@@ -21,6 +23,9 @@ def main():
     per = {"add": 3 * 4 * n, "copy": 2 * 4 * n}[kind]
     torch.cuda.synchronize()
     print(json.dumps({"ready": True}), flush=True)  # a sampler beside it starts from here
+    start_at = float(os.environ.get("HBM_STREAM_START_AT", "0"))  # several streams over one window
+    while time.time() < start_at:
+        time.sleep(0.001)
     t0 = time.perf_counter()
     done = 0
     while time.perf_counter() - t0 < secs:

@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 
 GPU_METRICS = ["fan_speed", "mem_free", "mem_used", "mem_total", "utilization", "mem_util", "temp", "power",
                # new (MI355X telemetry)
-               "hotspot_temp", "mem_temp", "gfx_clock", "mem_clock", "hbm_bw", "mfma_busy", "hbm_contention", "xgmi_read",
+               "hotspot_temp", "mem_temp", "gfx_clock", "mem_clock", "hbm_bw", "mfma_busy", "mfma_contention", "hbm_contention", "xgmi_read",
                "xgmi_write", "energy"]
 CPU_METRICS = ["mem_free", "mem_used", "mem_total", "utilization"]
 

@@ -9,7 +9,9 @@ import { LineChart, fmtNum } from "./chart.js";
 import { View, attempt, card, field, h, modal, pill, select, table } from "./ui.js";
 
 export const GPU_METRICS = {
-  utilization: ["GPU util", "%", 100], mem_util: ["HBM activity", "%", 100], mfma_busy: ["MFMA busy (probe)", "%", 100],
+  utilization: ["GPU util", "%", 100], mem_util: ["HBM activity", "%", 100], mfma_busy: ["MFMA busy (counters)", "%", 100],
+  mfma_contention: ["MFMA contention (probe)", "%", 100], gpu_busy: ["GPU busy (counters)", "%", 100],
+  mfma_tflops: ["MFMA TFLOP/s (counters)", " TF", null],
   hbm_bw: ["HBM bandwidth", " GB/s", null], hbm_contention: ["HBM contention (probe)", "%", 100],
   power: ["power", " W", null], energy: ["power (accumulator)", " W", null], temp: ["edge temp", " C", null],
   hotspot_temp: ["hotspot temp", " C", null], mem_temp: ["HBM temp", " C", null], mem_used: ["VRAM used", " MiB", null],
@@ -38,8 +40,12 @@ function gpuRow(uuid, g) {
     h("td", {}, g.index), h("td", { title: uuid }, (g.name || "GPU").replace("AMD Instinct ", "")),
     h("td", {}, bar(mv(m, "utilization")), " ", fmtNum(mv(m, "utilization")), "%"),
     h("td", {}, fmtNum(mv(m, "mem_used")), " / ", fmtNum(mv(m, "mem_total")), " MiB"),
-    h("td", {}, fmtNum(mv(m, "hbm_bw")), " GB/s"),
-    h("td", {}, mv(m, "mfma_busy") === null ? "-" : fmtNum(mv(m, "mfma_busy")) + "%"),
+    h("td", { title: "source: " + (mv(m, "hbm_bw_source") || "umc_activity") },
+      fmtNum(mv(m, "hbm_bw")), " GB/s", mv(m, "hbm_bw_source") === "partial" ? " (partial)" : ""),
+    // MFMA: the counter value where th-counters runs, else the probe's contention estimate (~)
+    mv(m, "mfma_busy") !== null ? h("td", { title: "SQ_VALU_MFMA_BUSY_CYCLES" }, fmtNum(mv(m, "mfma_busy")) + "%")
+      : h("td", { title: "probe contention, not busy cycles" },
+        mv(m, "mfma_contention") === null ? "-" : "~" + fmtNum(mv(m, "mfma_contention")) + "%"),
     h("td", {}, fmtNum(mv(m, "power")), " W"),
     h("td", {}, fmtNum(mv(m, "temp")), " / ", fmtNum(mv(m, "hotspot_temp")), " C"),
     h("td", {}, fmtNum(mv(m, "xgmi_read")), " / ", fmtNum(mv(m, "xgmi_write"))),

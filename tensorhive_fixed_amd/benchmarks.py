@@ -739,7 +739,7 @@ def monitoring_overhead(window_s: float = 20.0, train_rounds: int = 2, steps: in
                              "probe_agent_cpu_pct_of_one_core": round(100 * (a1 - a0) / wall, 2),
                              "probe_duty_pct": [((g.get("metrics") or {}).get("probe_duty") or {}).get("value")
                                                 for g in snap.values()],
-                             "mfma_busy_pct": [((g.get("metrics") or {}).get("mfma_busy") or {}).get("value")
+                             "mfma_contention_pct": [((g.get("metrics") or {}).get("mfma_contention") or {}).get("value")
                                                for g in snap.values()]}
         # tenant impact: alternate (a) nothing else, (b) the monitoring running, (c) the in-task HBM tool
         rates = {"alone": [], "with_monitoring": [], "with_task_hbm_tool": []}

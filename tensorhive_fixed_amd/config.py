@@ -295,6 +295,9 @@ class AmdMonitorConfig:
     counters_period_ms: int = 1000
     # tasks count their own HBM bytes (libthhbm via ROCP_TOOL_LIBRARIES, core/hbm.py)
     task_hbm_counters: bool = True
+    # remote nodes: "agent" (the node agent streams the full telemetry: probe + HBM files) or "th-smi"
+    remote_mode: str = "agent"
+    remote_agent: str = "python3 -m tensorhive_fixed_amd.agent"
 
 
 @dataclass
@@ -472,6 +475,8 @@ def load_config(directory: Path | str | None = None) -> Config:
             counters_enabled=main.bool("amd_monitor", "counters_enabled", False),
             counters_period_ms=main.int("amd_monitor", "counters_period_ms", 1000),
             task_hbm_counters=main.bool("amd_monitor", "task_hbm_counters", True),
+            remote_mode=main.str("amd_monitor", "remote_mode", "agent"),
+            remote_agent=main.str("amd_monitor", "remote_agent", "python3 -m tensorhive_fixed_amd.agent"),
         ),
         launcher=LauncherConfig(
             supervisor=main.str("launcher", "supervisor", "th-run"),

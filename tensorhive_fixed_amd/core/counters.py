@@ -6,6 +6,9 @@ line per period; :func:`derive` turns raw counter sums of one window into the me
 monitoring entry carries (``{value, unit}`` like every other metric):
 
 * ``gpu_busy``    -- GRBM_GUI_ACTIVE / GRBM_COUNT  (% of cycles the graphics engine was busy)
+* ``mfma_busy``   -- SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_COUNT / XCDs x SIMDs): the share of every
+  SIMD's cycles its matrix core was busy (the device-wide counterpart of the dispatch-PMC
+  "MFMA busy" of ``profiles/r03_gemm``; 8 XCDs x 1024 SIMDs on MI355X)
 * ``mfma_tflops`` -- SQ_INSTS_VALU_MFMA_MOPS_{BF16,F8,...} x 512 FLOP / window
 * ``hbm_read`` / ``hbm_write`` -- TCC EA request counts x request size / window (GB/s), only when
   the requested counters include them (they read ~0 in device-counting mode on gfx950).
@@ -32,21 +35,29 @@ MFMA_MOPS = ("SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_
 # MOPS counters (x512 FLOP) track a bf16 GEMM within 5 % of torch's own timing.  In device-counting
 # mode the TCC/EA request counters and SQ_WAVES read ~0 under a 5 TB/s copy, so HBM traffic is not
 # taken from counters (libthsmi's amdsmi memory activity is used instead).
-DEFAULT_COUNTERS = ("GRBM_GUI_ACTIVE", "GRBM_COUNT", "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F16",
-                    "SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_INSTS_VALU_MFMA_MOPS_F32")
+DEFAULT_COUNTERS = ("GRBM_GUI_ACTIVE", "GRBM_COUNT", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+                    "SQ_INSTS_VALU_MFMA_MOPS_F16", "SQ_INSTS_VALU_MFMA_MOPS_F8", "SQ_INSTS_VALU_MFMA_MOPS_F32")
+# SQ_VALU_MFMA_BUSY_CYCLES sums over every SIMD; GRBM counters sum over the XCDs (gfx950: 8 XCDs,
+# 32 CUs x 4 SIMDs each).  Read device-wide from th-counters' own process it matches the probe
+# validation loads (profiles/r04_probe/): the device counting service sees every tenant's SQ work.
+XCDS, SIMDS = 8, 1024
 
 
 def _m(value, unit):
     return {"value": value, "unit": unit}
 
 
-def derive(gpu: dict, window_ms: float) -> dict:
+def derive(gpu: dict, window_ms: float, xcds: int = XCDS, simds: int = SIMDS) -> dict:
     """One GPU's raw counter sums (``{"counters": {...}}``) -> dashboard metrics."""
     c = gpu.get("counters") or {}
     s = max(window_ms, 1e-3) / 1000.0
     out = {}
     if c.get("GRBM_COUNT"):
         out["gpu_busy"] = _m(round(100.0 * c.get("GRBM_GUI_ACTIVE", 0) / c["GRBM_COUNT"], 1), "%")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+            cycles = c["GRBM_COUNT"] / xcds  # elapsed shader-clock cycles of the window
+            busy = 100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (cycles * simds)
+            out["mfma_busy"] = _m(round(min(100.0, max(0.0, busy)), 1), "%")
     mops = [c[k] for k in MFMA_MOPS if k in c]
     if mops:
         out["mfma_tflops"] = _m(round(sum(mops) * MOPS_FLOP / s / 1e12, 1), "TFLOP/s")

@@ -57,7 +57,8 @@ class Daemon:
                 b = make_backend(kind, h, self.transports, am.stub_gpus, am.probe_enabled, am.probe_period,
                                  stream_ms=int(1000 * self.cfg.monitoring.update_interval),
                                  counters=am.counters_enabled, counters_period_ms=am.counters_period_ms,
-                                 task_hbm=am.task_hbm_counters)
+                                 task_hbm=am.task_hbm_counters, remote_mode=am.remote_mode,
+                                 remote_agent=am.remote_agent)
                 # one StubBackend / AmdSmiBackend instance is enough for all hosts of that kind
                 backends[h] = shared.setdefault(type(b).__name__, b) if isinstance(b, StubBackend) else b
         self.backends = backends

@@ -203,7 +203,7 @@ class UsageLoggingService(Service):
     """Per-reservation JSON logs, format of the reference (``UsageLoggingService.py:38-121``) plus
     extra MI355X metrics.  Cleanup action: 0 remove, 1 hide, 2 rename ``old_``."""
 
-    EXTRA = ("power", "hbm_bw", "mfma_busy", "xgmi_read", "xgmi_write")
+    EXTRA = ("power", "hbm_bw", "mfma_busy", "mfma_contention", "xgmi_read", "xgmi_write")
 
     def __init__(self, interval: float, log_dir: str, cleanup_action: int = 1):
         super().__init__("UsageLoggingService", interval)

@@ -6,16 +6,19 @@ call.  Backends:
 
 * :class:`AmdSmiBackend` -- the local node through ``native/lib/libthsmi.so`` (C++, amdsmi +
   /proc + KFD sysfs), augmented per GPU by the ``th-probe`` agent (the gfx950 probe kernel on
-  every device: ``mfma_busy``, ``hbm_contention``); ``hbm_bw`` (GB/s) comes from libthsmi's
+  every device: ``mfma_contention``, ``hbm_contention``) and the device counter sampler
+  (``th-counters``: ``mfma_busy`` from SQ_VALU_MFMA_BUSY_CYCLES, ``gpu_busy``, ``mfma_tflops``);
+  ``hbm_bw`` (GB/s) comes from libthsmi's
   calibrated ``mem_activity_acc`` rate.
-* :class:`RemoteBackend` -- other nodes: ``th-smi`` over the node transport, either one-shot or
-  as a persistent ``th-smi --stream MS`` over one multiplexed SSH channel (sub-second cadence
-  without a round trip per poll).
+* :class:`RemoteBackend` -- other nodes over one multiplexed SSH channel each: the node agent
+  (``agent.py``: the same AmdSmiBackend, probe agent and in-task HBM files on that node) or
+  ``th-smi --stream MS`` (sub-second cadence without a round trip per poll).
 * :class:`StubBackend` -- deterministic fake MI355X nodes (CPU-only hosts, tests, demos), with
   process injection and fault injection (host down / stalled).
 """
 from __future__ import annotations
 
+import copy
 import ctypes
 import json
 import logging
@@ -52,6 +55,20 @@ def entry_from_thsmi(host: str, doc: dict, extra_gpu_metrics: dict | None = None
     cpu = doc.get("cpu")
     return {"CPU": {f"CPU_{host}": {"name": f"CPU_{host}", "index": 0, "metrics": cpu}} if cpu else None,
             "GPU": gpus}
+
+
+def apply_task_hbm(entry: dict, pattern: str | None = None) -> dict:
+    """Merge the node's in-task HBM counter files (``core/hbm.py``) into an infrastructure entry,
+    in place: counted GPUs get ``hbm_read/hbm_write/hbm_bw`` with ``hbm_bw_source`` ``counters``
+    or ``partial``; the others keep their estimate, labelled ``umc_activity``."""
+    from . import hbm
+
+    gpus = list((entry.get("GPU") or {}).values())
+    rates = hbm.read_rates(pattern) if pattern else hbm.read_rates()
+    counted = hbm.metrics_for(gpus, rates)
+    for g in gpus:
+        g.setdefault("metrics", {}).update(counted.get(g.get("index"), {"hbm_bw_source": _metric("umc_activity", "")}))
+    return entry
 
 
 class TelemetryBackend:
@@ -148,14 +165,10 @@ class AmdSmiBackend(TelemetryBackend):
                 m = by_kfd.get(g.get("kfd_id"))
                 if m:
                     extra.setdefault(g["index"], {}).update(m)
+        entry = entry_from_thsmi(host, doc, extra or None)
         if self.task_hbm:  # HBM bytes counted inside the tasks themselves (core/hbm.py)
-            from . import hbm
-
-            counted = hbm.metrics_for(doc.get("gpus", []), hbm.read_rates())
-            for g in doc.get("gpus", []):
-                extra.setdefault(g["index"], {}).update(
-                    counted.get(g["index"], {"hbm_bw_source": _metric("umc_activity", "")}))
-        return entry_from_thsmi(host, doc, extra or None)
+            apply_task_hbm(entry)
+        return entry
 
     def topology(self, host: str) -> dict | None:
         return self._call(self.lib.thsmi_topology_json)
@@ -210,12 +223,18 @@ class GpuProbe:
     streams one JSON line per period; this reader keeps the newest line and, per GPU (matched by
     PCI BDF, else HIP index), derives::
 
-        mfma_busy      = max(1 - t_mfma_idle / t_mfma, 1 - latency_idle / latency)  (%)
+        mfma_contention = max(1 - t_mfma_idle / t_mfma, 1 - latency_idle / latency)  (%)
         hbm_contention = 1 - bw / bw_idle                                           (%)
         probe_duty     = probe kernel time / period                                 (%)
 
     (two ways a tenant shows up: it shares SIMDs with the probe, or it holds every CU so the
-    probe waits to be dispatched).  Idle references come from :class:`ProbeBaseline`."""
+    probe waits to be dispatched).  Idle references come from :class:`ProbeBaseline`.
+
+    ``mfma_contention`` is how much a tenant slows the probe's MFMA work, NOT the share of cycles
+    the matrix cores are busy: against SQ_VALU_MFMA_BUSY_CYCLES it read 71 vs 70 % under a
+    hipBLASLt GEMM (one wave per SIMD, the probe waits for dispatch) but 32 vs 52 % under the flash
+    backward (two workgroups per CU, the probe co-resides), ``profiles/r04_probe/``.  The counter
+    value is reported as ``mfma_busy`` by the device counter sampler (``core/counters.py``)."""
 
     def __init__(self, period: float = 1.0, n_wg: int = 8, mfma_iters: int = 512, binary: str | None = None,
                  devices: str = "all", idle_util: float = 2.0, cmd: list[str] | None = None):
@@ -328,7 +347,7 @@ class GpuProbe:
             busy = max(busy_chain, busy_wait) * 100 if s["mfma_us"] > 0 else None
             share = max(0.0, 1.0 - s["bw"] / b0) * 100 if b0 > 0 else None
             out[g["index"]] = {
-                "mfma_busy": _metric(None if busy is None else round(busy, 1), "%"),
+                "mfma_contention": _metric(None if busy is None else round(busy, 1), "%"),
                 "hbm_contention": _metric(None if share is None else round(share, 1), "%"),
                 "probe_xcds": _metric(s["xcds"], ""),
                 "probe_duty": _metric(round(100.0 * s["kernel_us"] * 1e-6 / self.period, 4), "%"),
@@ -348,25 +367,76 @@ class GpuProbe:
                 self._proc.kill()
 
 
+DEFAULT_AGENT = "python3 -m tensorhive_fixed_amd.agent"
+
+
 class RemoteBackend(TelemetryBackend):
-    """th-smi on other nodes via their transport (one-shot or persistent stream)."""
+    """Other nodes through their transport.
+
+    * ``mode="agent"`` (default): the node agent (``agent.py``) streams complete infrastructure
+      entries over ONE multiplexed SSH channel -- libthsmi metrics and processes, the node's own
+      probe agent (``mfma_contention`` / ``hbm_contention``), its device counters (``mfma_busy``)
+      and its authenticated in-task HBM counter
+      files -- i.e. the same telemetry the daemon's own node gets.  If the agent cannot run on a
+      node (not installed: it exits before its first line, twice), the backend falls back to
+      th-smi for that node.
+    * ``mode="th-smi"``: ``th-smi --stream MS`` (or one-shot ``th-smi --json`` without
+      ``stream_ms``): amdsmi metrics and processes only.
+
+    A stream whose newest line is older than ``stale_s`` reports the node as down (None)."""
 
     name = "remote"
 
-    def __init__(self, transports, th_smi: str = "th-smi", stream_ms: int | None = None):
+    def __init__(self, transports, th_smi: str = "th-smi", stream_ms: int | None = None, mode: str = "agent",
+                 agent_cmd: str = DEFAULT_AGENT, agent_args: str = "", stale_s: float | None = None):
         self.transports = transports
         self.th_smi = th_smi
         self.stream_ms = stream_ms
-        self._latest: dict[str, tuple[float, dict]] = {}
+        self.mode = mode
+        self.agent_cmd = agent_cmd or DEFAULT_AGENT
+        self.agent_args = agent_args
+        self.stale_s = stale_s if stale_s is not None else max(5.0, 4 * (stream_ms or 1000) / 1000.0)
+        self._latest: dict[str, tuple[float, dict, str]] = {}
         self._procs: dict[str, subprocess.Popen] = {}
+        self._modes: dict[str, str] = {}
+        self._agent_failures: dict[str, int] = {}
+        self._started: dict[str, float] = {}
+        self.errors: dict[str, str] = {}
         self._lock = threading.Lock()
 
-    def _start_stream(self, host: str) -> None:
+    def node_mode(self, host: str) -> str:
+        return self._modes.get(host, self.mode)
+
+    def _command(self, host: str) -> str:
+        ms = int(self.stream_ms or 1000)
+        if self.node_mode(host) == "agent":
+            return f"exec {self.agent_cmd} --stream {ms} --host {host} {self.agent_args}".strip()
+        return f"exec {self.th_smi} --stream {ms}"
+
+    def _argv(self, host: str) -> list[str]:
         t = self.transports.get(host)
-        argv = t.base_argv() + [f"{self.th_smi} --stream {int(self.stream_ms)}"] if hasattr(t, "base_argv") else \
-            ["bash", "-c", f"{self.th_smi} --stream {int(self.stream_ms)}"]
-        p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, bufsize=1)
+        cmd = self._command(host)
+        if hasattr(t, "stream_argv"):
+            return t.stream_argv(cmd)
+        if hasattr(t, "base_argv"):
+            return t.base_argv() + [cmd]
+        return ["bash", "-c", cmd]
+
+    def _start_stream(self, host: str) -> None:
+        prev = self._procs.get(host)
+        if prev is not None and self.node_mode(host) == "agent" and host in self._started:
+            got_line = self._latest.get(host, (0.0, None, ""))[0] >= self._started[host]
+            if not got_line:  # died before its first line: not installed / cannot start
+                n = self._agent_failures[host] = self._agent_failures.get(host, 0) + 1
+                if n >= 2:
+                    log.warning("node agent unavailable on %s (%s); falling back to th-smi", host,
+                                self.errors.get(host, "no output"))
+                    self._modes[host] = "th-smi"
+        p = subprocess.Popen(self._argv(host), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, bufsize=1)
         self._procs[host] = p
+        self._started[host] = time.time()
+        mode = self.node_mode(host)
+        err = StderrTail(p.stderr, name=f"telemetry-stderr-{host}")
 
         def reader():
             for line in p.stdout:
@@ -374,10 +444,20 @@ class RemoteBackend(TelemetryBackend):
                     doc = json.loads(line)
                 except json.JSONDecodeError:
                     continue
+                if mode == "agent":
+                    if doc.get("error"):
+                        self.errors[host] = doc["error"]
+                        continue
+                    doc = doc.get("entry")
+                    if doc is None:
+                        continue
                 with self._lock:
-                    self._latest[host] = (time.time(), doc)
+                    self._latest[host] = (time.time(), doc, mode)
+            p.wait()
+            if p.returncode not in (0, -15, None):
+                self.errors.setdefault(host, f"exit {p.returncode}: " + err.text(limit=300))
 
-        threading.Thread(target=reader, name=f"th-smi-stream-{host}", daemon=True).start()
+        threading.Thread(target=reader, name=f"telemetry-stream-{host}", daemon=True).start()
 
     def sample(self, host: str) -> dict | None:
         if self.stream_ms:
@@ -386,7 +466,20 @@ class RemoteBackend(TelemetryBackend):
                 self._start_stream(host)
             with self._lock:
                 got = self._latest.get(host)
-            return entry_from_thsmi(host, got[1]) if got else None
+            if not got or time.time() - got[0] > self.stale_s:
+                return None
+            ts, doc, mode = got
+            return copy.deepcopy(doc) if mode == "agent" else entry_from_thsmi(host, doc)
+        if self.node_mode(host) == "agent":
+            r = self.transports.run(host, f"{self.agent_cmd} --once --host {host} {self.agent_args}".strip(),
+                                    timeout=60)
+            try:
+                doc = json.loads(r.stdout.strip().splitlines()[-1]) if r.ok else None
+            except (json.JSONDecodeError, IndexError):
+                doc = None
+            if doc and doc.get("entry") is not None:
+                return doc["entry"]
+            self._modes[host] = "th-smi"  # one-shot mode: fall back at the first failure
         r = self.transports.run(host, f"{self.th_smi} --json", timeout=15)
         if not r.ok:
             return None
@@ -397,7 +490,13 @@ class RemoteBackend(TelemetryBackend):
 
     def close(self) -> None:
         for p in self._procs.values():
-            p.terminate()
+            if p.poll() is None:
+                p.terminate()
+        for p in self._procs.values():
+            try:
+                p.wait(5)
+            except subprocess.TimeoutExpired:
+                p.kill()
 
 
 class StubBackend(TelemetryBackend):
@@ -455,6 +554,10 @@ class StubBackend(TelemetryBackend):
                         "xgmi_read": _metric(0.0, "GB/s"), "xgmi_write": _metric(0.0, "GB/s"),
                         "energy": _metric(180 + util * 8, "W"),  # accumulator-derived power, as libthsmi
                         "hbm_bw": _metric(round(util * 0.6 * 102.0, 1), "GB/s"),  # umc % x calibrated GB/s
+                        # the probe-derived keys a real node carries (scripted: busy GPUs read ~util)
+                        "mfma_busy": _metric(round(util * 0.6, 1), "%"),
+                        "mfma_contention": _metric(round(util * 0.85, 1), "%"),
+                        "hbm_contention": _metric(round(util * 0.5, 1), "%"),
                     },
                     "processes": procs,
                 }
@@ -470,9 +573,19 @@ class StubBackend(TelemetryBackend):
                                     for j in range(n)]} for i in range(n)]}
 
 
+def agent_args(probe: bool, probe_period: float, counters: bool, counters_period_ms: int, task_hbm: bool) -> str:
+    """The node agent's switches matching the daemon's ``[amd_monitor]`` settings."""
+    a = ["--probe" if probe else "--no-probe", f"--probe-period {probe_period:g}",
+         "--task-hbm" if task_hbm else "--no-task-hbm"]
+    if counters:
+        a += ["--counters", f"--counters-period-ms {int(counters_period_ms)}"]
+    return " ".join(a)
+
+
 def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, probe: bool = False,
                  probe_period: float = 1.0, stream_ms: int | None = None, counters: bool = False,
-                 counters_period_ms: int = 1000, task_hbm: bool = True) -> TelemetryBackend:
+                 counters_period_ms: int = 1000, task_hbm: bool = True, remote_mode: str = "agent",
+                 remote_agent: str = DEFAULT_AGENT) -> TelemetryBackend:
     """Pick a backend for ``host``: ``auto`` = amdsmi for the local node when /dev/kfd exists,
     remote th-smi for ssh nodes, stub otherwise."""
     spec_local = transports is None or getattr(transports.transports.get(host), "__class__", None).__name__ == "LocalTransport"
@@ -482,5 +595,6 @@ def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, prob
         return AmdSmiBackend(probe=probe, probe_period=probe_period, counters=counters,
                              counters_period_ms=counters_period_ms, task_hbm=task_hbm)
     if kind == "remote" or (kind == "auto" and not spec_local):
-        return RemoteBackend(transports, stream_ms=stream_ms)
+        return RemoteBackend(transports, stream_ms=stream_ms, mode=remote_mode, agent_cmd=remote_agent,
+                             agent_args=agent_args(probe, probe_period, counters, counters_period_ms, task_hbm))
     return StubBackend(stub_gpus)

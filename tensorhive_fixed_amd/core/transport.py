@@ -77,6 +77,10 @@ class LocalTransport(Transport):
             log.debug("local transport cannot switch to %s (not root); running as %s", user, me)
         return ["bash", "-c", command]
 
+    def stream_argv(self, command: str, user: str | None = None) -> list[str]:
+        """argv of a long-running command whose stdout the caller reads (telemetry streams)."""
+        return self._argv(command, user or self.user)
+
     def run(self, command, timeout=None, user=None, env=None) -> Result:
         try:
             p = subprocess.run(self._argv(command, user or self.user), capture_output=True, text=True,
@@ -109,6 +113,10 @@ class SSHTransport(Transport):
         if self.proxy:
             argv += ["-J", f"{self.proxy['proxy_user']}@{self.proxy['proxy_host']}:{self.proxy.get('proxy_port', 22)}"]
         return argv + [f"{u}@{self.host}"]
+
+    def stream_argv(self, command: str, user: str | None = None) -> list[str]:
+        """argv of a long-running remote command over the ControlMaster channel (telemetry streams)."""
+        return self.base_argv(user) + [command]
 
     def run(self, command, timeout=None, user=None, env=None) -> Result:
         if env:

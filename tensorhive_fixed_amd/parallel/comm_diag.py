@@ -93,7 +93,9 @@ def parse_rccl_init(text: str) -> dict:
         if m:
             out["thread_thresholds"] = m.group(1).strip()
         if " WARN " in f" {line} ":
-            out["warnings"].append(line[-300:])
+            msg = line.split(" WARN ", 1)[1].strip()[:200]
+            if msg not in out["warnings"] and len(out["warnings"]) < 8:  # unique messages only
+                out["warnings"].append(msg)
         # one example of each informative line, without the per-rank prefix
         body = line.split(" INFO ", 1)[-1]
         if _KEEP.search(body) and body not in seen and len(out["lines"]) < 24:

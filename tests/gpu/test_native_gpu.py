@@ -133,7 +133,7 @@ def test_daemon_with_local_amdsmi_backend(tmp_path, monkeypatch):
                 break
             time.sleep(0.1)
         gpus = snap.data["localhost"]["GPU"]
-        assert gpus and all("mfma_busy" in g["metrics"] for g in gpus.values())
+        assert gpus and all("mfma_contention" in g["metrics"] for g in gpus.values())
     finally:
         d.shutdown()
         C.set_config(None)

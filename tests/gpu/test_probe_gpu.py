@@ -3,7 +3,7 @@
 The ``th-probe`` agent runs the gfx950 probe kernel on EVERY GPU of the node; the daemon's
 monitor (this process, with the agent and th-counters as its children) is never listed as a
 tenant, so it neither raises a protection violation on a reserved GPU nor makes a GPU look busy
-to the allocator; ``mfma_busy`` is reported for every index libthsmi lists and rises under a
+to the allocator; ``mfma_contention`` is reported for every index libthsmi lists and rises under a
 tenant GEMM on the LAST device (device 0 on a one-GPU box)."""
 import datetime
 import json
@@ -66,7 +66,7 @@ def test_probe_busy_rises_under_a_tenant_gemm_on_the_last_device():
         def busy():
             gpus = b.sample("localhost")["GPU"]
             g = next(g for g in gpus.values() if g["index"] == dev)
-            return g["metrics"]["mfma_busy"]["value"], g["metrics"]["probe_baseline"]["value"]
+            return g["metrics"]["mfma_contention"]["value"], g["metrics"]["probe_baseline"]["value"]
 
         idle = []
         for _ in range(12):
@@ -85,7 +85,7 @@ def test_probe_busy_rises_under_a_tenant_gemm_on_the_last_device():
             p.wait(timeout=120)
         idle_med = sorted(idle)[len(idle) // 2]
         busy_med = sorted(loaded)[len(loaded) // 2]
-        print(f"device {dev}: probe mfma_busy idle median {idle_med:.1f} %, under GEMM {busy_med:.1f} %")
+        print(f"device {dev}: probe mfma_contention idle median {idle_med:.1f} %, under GEMM {busy_med:.1f} %")
         assert idle_med < 25.0, idle
         assert busy_med >= idle_med + 30.0, (idle, loaded)
         assert b.probe.baselines, "baselines were learned"
@@ -94,7 +94,7 @@ def test_probe_busy_rises_under_a_tenant_gemm_on_the_last_device():
 
 
 def test_monitor_is_never_its_own_tenant(cfg, tables, new_user):
-    """Probe on: the daemon and its helpers are absent from every process list, mfma_busy is
+    """Probe on: the daemon and its helpers are absent from every process list, mfma_contention is
     reported for every GPU, a reserved GPU 0 raises no violation, an auto:1 job may get GPU 0."""
     from tensorhive_fixed_amd.core import allocation
     from tensorhive_fixed_amd.core.daemon import Daemon
@@ -122,7 +122,7 @@ def test_monitor_is_never_its_own_tenant(cfg, tables, new_user):
         assert listed == list(range(_n_devices()))
         for g in gpus.values():
             assert not {p["pid"] for p in g["processes"]} & own, g["processes"]
-            assert g["metrics"]["mfma_busy"]["value"] is not None, g["metrics"]
+            assert g["metrics"]["mfma_contention"]["value"] is not None, g["metrics"]
             assert g["metrics"]["probe_duty"]["value"] < 0.1
         uuid0 = next(u for u, g in gpus.items() if g["index"] == 0)
         Resource(id=uuid0, name="MI355X", hostname=host).save()

@@ -94,12 +94,13 @@ host:1:1 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC
 host:1:1 [0] NCCL INFO threadThresholds 8/8/64 | 64/8/64 | 512 | 512
 host:1:1 [0] NCCL INFO 32 coll channels, 32 collnet channels, 0 nvls channels, 32 p2p channels, 32 p2p channels per peer
 host:1:1 [0] NCCL WARN something odd
+[2026-10-17 12:58:03] host:1:2 [0] /src/init.cc:161 NCCL WARN something odd
 """
     d = parse_rccl_init(log)
     assert d["library"] == "RCCL" and d["version"] == "2.22.3+hip7.0" and d["nranks"] == 8
     assert d["channels"] == 32 and d["coll_channels"] == 32 and d["p2p_channels"] == 32 and d["trees"] == 1
     assert d["transports"] == {"P2P/IPC": 2} and d["p2p_chunksize"] == 524288
-    assert d["thread_thresholds"].startswith("8/8/64") and len(d["warnings"]) == 1
+    assert d["thread_thresholds"].startswith("8/8/64") and d["warnings"] == ["something odd"]  # deduplicated
 
 
 def test_prepare_rccl_log_respects_user_settings(monkeypatch, tmp_path):

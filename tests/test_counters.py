@@ -19,6 +19,15 @@ def test_derive_units():
     assert derive({"counters": {}}, 100.0) == {}
 
 
+def test_derive_mfma_busy_from_sq_cycles():
+    # 100 k elapsed cycles per XCD (GRBM sums the 8 XCDs), every one of 1024 SIMDs busy 52 % of them
+    g = {"counters": {"GRBM_GUI_ACTIVE": 8e5, "GRBM_COUNT": 8e5, "SQ_VALU_MFMA_BUSY_CYCLES": 0.52 * 1e5 * 1024}}
+    assert derive(g, 50.0)["mfma_busy"] == {"value": 52.0, "unit": "%"}
+    g["counters"]["SQ_VALU_MFMA_BUSY_CYCLES"] = 3e9  # clamped: never above 100 %
+    assert derive(g, 50.0)["mfma_busy"]["value"] == 100.0
+    assert "mfma_busy" not in derive({"counters": {"GRBM_COUNT": 10, "GRBM_GUI_ACTIVE": 5}}, 50.0)
+
+
 def test_counter_stream_reads_lines(tmp_path):
     line = json.dumps({"ts_ns": 1, "window_ms": 100, "gpus": [
         {"kfd_id": 1234, "bdf": "0000:05:00.0", "counters": {"GRBM_GUI_ACTIVE": 5, "GRBM_COUNT": 10}}]})

@@ -62,8 +62,8 @@ def test_probe_stream_derives_per_gpu_metrics(tmp_path):
             time.sleep(0.05)
         last = seen[max(seen)]
         assert set(last) == {0, 1}
-        assert last[0]["mfma_busy"]["value"] == 0.0
-        assert abs(last[1]["mfma_busy"]["value"] - 60.0) < 0.5  # 1 - 10/25
+        assert last[0]["mfma_contention"]["value"] == 0.0
+        assert abs(last[1]["mfma_contention"]["value"] - 60.0) < 0.5  # 1 - 10/25
         assert last[1]["probe_baseline"]["value"] == "idle"
         assert last[0]["probe_xcds"]["value"] == 4
         assert last[0]["probe_duty"]["value"] == round(100 * 30e-6 / 0.1, 4)  # (10+20) us per 100 ms
