@@ -1,6 +1,9 @@
 """gfx950 NT GEMM (ops/csrc/gemm_nt.hip) vs hipBLASLt (torch.mm) on the Llama-3-8B forward and
-input-gradient shapes (MB 8 x 4096 tokens): exactness vs torch first, then interleaved timing
-(median of 15 per arm, 3 rounds).  One JSON line per shape."""
+input-gradient shapes (MB 8 x 4096 tokens): fp32 check first, then interleaved timing on random
+operands (median of 15 launches per arm, 3 rounds, best round).  One JSON line per shape.
+
+    python scripts/bench_gemm_nt.py [SHAPE ...]
+"""
 import json
 import statistics
 import sys
@@ -9,11 +12,12 @@ import torch
 
 sys.path.insert(0, ".")
 from tensorhive_fixed_amd.ops import _lib  # noqa: E402
-from tensorhive_fixed_amd.ops.gemm_nt import gemm_nt_  # noqa: E402
+from tensorhive_fixed_amd.ops.gemm_nt import gemm_nt_, usable  # noqa: E402
 
-T, D, F = 32768, 4096, 14336
+T, D, F, V = 32768, 4096, 14336, 128256
 SHAPES = [("wqkv.fwd", T, 6144, D), ("wo.fwd", T, D, D), ("w13.fwd", T, 2 * F, D), ("w2.fwd", T, D, F),
-          ("wqkv.dgrad", T, D, 6144), ("w13.dgrad", T, D, 2 * F), ("w2.dgrad", T, F, D)]
+          ("wqkv.dgrad", T, D, 6144), ("wo.dgrad", T, D, D), ("w13.dgrad", T, D, 2 * F), ("w2.dgrad", T, F, D),
+          ("w13.wgrad", 2 * F, D, T), ("head.fwd", 4096, V, D), ("head.dgrad", 4096, D, V)]
 
 
 def timed(fn, iters=15):
@@ -30,43 +34,37 @@ def timed(fn, iters=15):
 
 def main():
     _lib.load()
+    want = set(sys.argv[1:])
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    # exactness on a small problem of every kind first (fp32 reference)
     for (M, N, K) in ((512, 512, 64), (256, 768, 4096), (1024, 256, 14336)):
         a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
         b = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         gemm_nt_(a, b, c)
         ref = a.float() @ b.float().t()
-        c16 = torch.empty_like(c)
-        gemm_nt_(a, b, c16, mfma16=True)
-        rel16 = ((c16.float() - ref).norm() / ref.norm()).item()
-        assert rel16 < 1e-2, rel16
         rel = ((c.float() - ref).norm() / ref.norm()).item()
-        c0 = c.clone()
-        gemm_nt_(a, b, c, accumulate=True)
-        rel2 = ((c.float() - (c0.float() + ref)).norm() / ref.norm()).item()
-        print(json.dumps({"check": [M, N, K], "rel_err": rel, "rel_err_beta": rel2}), flush=True)
-        assert rel < 1e-2 and rel2 < 2e-2
+        print(json.dumps({"check": [M, N, K], "rel_err": rel}), flush=True)
+        assert rel < 1e-2, rel
     for name, M, N, K in SHAPES:
+        if want and name not in want:
+            continue
         a = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=g)
         b = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=g)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         c2 = torch.empty_like(c)
+        assert usable(a, b, c)
         gemm_nt_(a, b, c)
         torch.mm(a, b.t(), out=c2)
         diff = ((c.float() - c2.float()).norm() / c2.float().norm()).item()
-        res = {"nt": [], "nt16": [], "hipblaslt": []}
+        res = {"nt": [], "hipblaslt": []}
         for _ in range(3):
             res["nt"].append(timed(lambda: gemm_nt_(a, b, c)))
-            res["nt16"].append(timed(lambda: gemm_nt_(a, b, c, mfma16=True)))
             res["hipblaslt"].append(timed(lambda: torch.mm(a, b.t(), out=c2)))
         fl = 2.0 * M * N * K
-        nt, nt16, hb = min(res["nt"]), min(res["nt16"]), min(res["hipblaslt"])
+        nt, hb = min(res["nt"]), min(res["hipblaslt"])
         print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "nt_ms": round(nt, 4), "hipblaslt_ms": round(hb, 4),
-                          "nt_tflops": round(fl / nt / 1e9), "nt16_tflops": round(fl / nt16 / 1e9),
-                          "hipblaslt_tflops": round(fl / hb / 1e9),
+                          "nt_tflops": round(fl / nt / 1e9), "hipblaslt_tflops": round(fl / hb / 1e9),
                           "speedup": round(hb / nt, 3), "rel_diff_vs_hipblaslt": diff}), flush=True)
         del a, b, c, c2
     return 0

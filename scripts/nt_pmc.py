@@ -16,7 +16,7 @@ a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
 b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
 c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(5):
-    gemm_nt_(a, b, c, mfma16=True, variant=int(os.environ.get("NT_VARIANT", "4")))
+    gemm_nt_(a, b, c)
 for _ in range(5):
     torch.mm(a, b.t(), out=c)
 torch.cuda.synchronize()

@@ -95,10 +95,10 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 
 
 # launch flags of the backward (th_flash_attn_bwd), A/B aids: bit0 q-major dQ order; bit1 / bit2
-# fused dK/dV order / priority; bit3 the fused dK/dV kernel instead of a paired one; bit5
-# register-staged K/V tiles in dQ (and in dK|dV); bit6 register-staged Q/dO tiles in the 8-wave
-# paired dK|dV kernel; bit7 its one-barrier-per-tile variant (profiles/r02_flash: slower); bit8 the
-# 8-wave paired kernel instead of the default half-width one (profiles/r03_flash)
+# fused dK/dV order / priority; bit3 the fused register-staged dK/dV kernel instead of the paired
+# half-width one; bit5 register-staged K/V tiles in dQ and the fused dK/dV kernel (the path
+# sequences whose LDS-DMA offsets overflow 32 bits take by themselves).  The 8-wave paired kernels
+# of rounds 2-3 (old bits 6-8) are retired: profiles/r03_flash/retired_kc_kernels.patch
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", "0"))
 
 

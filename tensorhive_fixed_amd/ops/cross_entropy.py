@@ -16,6 +16,7 @@ import torch
 
 from . import _lib
 from .gemm_tn import gemm_tn_, supported as gemm_tn_supported
+from .gemm_nt import nt_mm
 from .linear import _DGRAD_NT
 from .transpose import transpose
 
@@ -75,9 +76,12 @@ class _LinearCE(torch.autograd.Function):
         w_kn = transpose(w).t() if (h2.is_cuda and _DGRAD_NT) else w
         for i, s0 in enumerate(range(0, T, chunk)):
             hc = h2[s0: s0 + chunk]
-            logits = torch.mm(hc, w.t())
+            logits = nt_mm(hc, w) if hc.is_cuda else torch.mm(hc, w.t())
             loss_sum += ce_rows_(logits, t[s0: s0 + chunk], scale, ignore_index).sum()
-            torch.mm(logits, w_kn, out=dh[s0: s0 + chunk])
+            if h2.is_cuda and _DGRAD_NT:
+                nt_mm(logits, w_kn.t(), out=dh[s0: s0 + chunk])
+            else:
+                torch.mm(logits, w_kn, out=dh[s0: s0 + chunk])
             if mg is not None:
                 # dW += dlogitsᵀ hc; with TH_HEAD_WGRAD_NT both operands are transposed first so the
                 # GEMM runs in the K-contiguous form

@@ -823,526 +823,32 @@ __global__ __launch_bounds__(B_THREADS, 2) void fa_bwd_dkv_kernel(
 // ------------------------------------------------------------ paired key-centric dK | dV kernel
 // The fused dK/dV kernel above needs 128 accumulator VGPRs (dK and dV) and so cannot keep its
 // K/V operands in registers: every S / dP MFMA reads BOTH operands from LDS, and the K/V block
-// costs 128 KB of LDS.  Here a workgroup of 8 waves covers 128 keys, and each 32-key slice is
-// owned by a PAIR of waves with one accumulator each:
-//   dV wave (4-7):  phase 1  S = Q K^T -> P (registers + LDS exchange)   phase 2  dV^T += dO^T P
-//   dK wave (0-3):  phase 1  dP = dO V^T                                 phase 2  dS = P (dP - delta),
-//                                                                                 dK^T += Q^T dS
+// costs 128 KB of LDS.  In the paired kernels each 32-key slice is owned by a PAIR of waves with
+// one accumulator each:
+//   dV wave:  phase 1  S = Q K^T -> P (registers + LDS exchange)   phase 2  dV^T += dO^T P
+//   dK wave:  phase 1  dP = dO V^T                                 phase 2  dS = P (dP - delta),
+//                                                                           dK^T += Q^T dS
 // Both roles run 16 + 16 MFMAs per 64-query tile (balanced, no GEMM recomputed), hold only 64
 // accumulator VGPRs, keep their K (dV wave) or V (dK wave) fragments in registers for the whole
 // kernel, and read one MFMA operand per instruction from LDS (like the dQ kernel).  P crosses
-// from the dV wave to its partner as f32 through an 8 KB lane-linear LDS slot (conflict-free
-// ds_write/read_b128), one barrier between the phases.  The pair shares one staged Q/dO tile
+// from the dV wave to its partner through a lane-linear LDS slot (conflict-free wide
+// ds_write/read), one barrier between the phases.  The pair shares one staged Q/dO tile
 // (the dK waves stage Q + lse + delta, the dV waves dO).
 // B4 S4096 32/8 heads: backward 2.64 -> 2.29 ms against the fused kernel (profiles/r01_flash_v3).
 // (Measured on the way: one role per workgroup streaming the tile twice = no faster than the
 // fused kernel; paired roles that each recompute S = -9 %; LDS double-buffering = no change.)
-constexpr int C_BK = 128, C_BQ = 64, KC_TILE = 2 * C_BQ * 256 + 2 * C_BQ * 4;
-
-template <bool DK, bool DMA>
-__device__ __forceinline__ void kc_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
-                                        const float* __restrict__ LSE, const float* __restrict__ Dl,
-                                        const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
-                                        char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
-                                        long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  // role-local thread id: waves 0-3 are the dK role, 4-7 the dV role of the same 128 keys
-  const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-  // tile buffers [Q | dO | lse | delta] (two with DMA), then the P exchange of wave pair w:
-  // [half][4 x float4][lane], 8 KB
-  float4v* pbuf = reinterpret_cast<float4v*>(smem + (DMA ? 2 : 1) * KC_TILE + w * 8192);
-  const int k0 = kblk0 + 32 * w;
-  const int key = k0 + c32;
-  // dK role: V fragments (dP = dO V^T); dV role: K fragments (S = Q K^T)
-  const ushort* fb = DK ? Vb : Kb;
-  // Row constants as the initial accumulators: the tile buffer holds -lse2 and -delta per query,
-  // the S chain (dV role) starts from -lse2 with K prescaled by softmax_scale * log2(e) and the dP
-  // chain (dK role) from -delta, so p = exp2(S') and dS = p * dP' (no fma / sub per score).
-  bf16x8 kf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    ushort8 u = key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0);
-    if (!DK) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
-    }
-    kf[s] = as_bf(u);
-  }
-  f32x16 acc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
-
-  const int nqt = (S + C_BQ - 1) / C_BQ;
-  const int qt0 = causal ? kblk0 / C_BQ : 0;
-  const int per_head = nqt - qt0;
-  const int total = G * per_head;
-  ushort8 xr[4];  // the dK role stages the Q tile (+ lse, delta), the dV role the dO tile
-  float lr = 0.f, dr = 0.f;
-  int pf_h = 0, pf_t = 0, cur_t = 0;
-  auto prefetch = [&](int h_i, int t_i) {
-    const int hq = hk * G + h_i;
-    const int qq0 = (qt0 + t_i) * C_BQ;
-    if (DK)
-      stage_load<4>(xr, Q + b * bs + (long)hq * HD, ld, qq0, S, tid);
-    else
-      stage_load<4>(xr, dO + b * bso + (long)hq * HD, ldo, qq0, S, tid);
-    if (DK && tid < C_BQ) {
-      const int qq = qq0 + tid;
-      const long st = ((long)b * Hq + hq) * S;
-      const int qc = min(qq, S - 1);
-      lr = LSE[st + qc];  // LOG2E-scaled when stored
-      dr = Dl[st + qc];
-      lr = qq < S ? lr : INFINITY;  // rows past S: P = 0 exactly
-      dr = qq < S ? dr : 0.f;
-    }
-  };
-  // DMA mode: the role's 4 waves DMA its 16 KB image (Q for dK, dO for dV) one tile ahead into
-  // the other buffer; lse / delta still go through registers, loaded two tiles ahead
-  unsigned rc[4];
-  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto dma_tile = [&](int h_i, int t_i, int buf) {
-    const int hq = hk * G + h_i;
-    const int qq0 = (qt0 + t_i) * C_BQ;
-    const ushort* base = DK ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
-    const long ldx = DK ? ld : ldo;
-    const unsigned img = lds0 + buf * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 4096;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
-      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
-    }
-  };
-  // raw loads only: the row-validity selects happen in write_ld, so nothing consumes the loaded
-  // values right after their issue (a use there would make the compiler wait -- and the hardware
-  // vmcnt also counts the tile DMA issued just before)
-  int lq = 0;
-  auto load_ld = [&](int h_i, int t_i) {
-    if (DK && tid < C_BQ) {
-      const int hq = hk * G + h_i;
-      lq = (qt0 + t_i) * C_BQ + tid;
-      const long st = ((long)b * Hq + hq) * S;
-      const int qc = min(lq, S - 1);
-      lr = LSE[st + qc];
-      dr = Dl[st + qc];
-    }
-  };
-  auto write_ld = [&](int buf) {
-    if (DK && tid < C_BQ) {
-      float* l = reinterpret_cast<float*>(smem + buf * KC_TILE + 2 * C_BQ * 256);
-      // negated (initial accumulators); rows past S: -inf -> P = 0 exactly
-      l[tid] = DMA ? (lq < S ? -lr * LOG2E : -INFINITY) : -lr * LOG2E;
-      l[C_BQ + tid] = DMA ? (lq < S ? -dr : 0.f) : -dr;
-    }
-  };
-  int lh = 0, lt = 0;  // tile of the lse / delta registers (DMA mode)
-  auto adv = [&](int& hh, int& tt) {
-    if (++tt == per_head) { tt = 0; ++hh; }
-  };
-  if (DMA) {
-    // retire the K/V fragment loads with a wait the compiler sees (see the dQ kernel)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) rc[u] = img_rc(wu * 4096 + u * 1024 + lane * 16);
-    if (total > 0) {
-      load_ld(0, 0);
-      write_ld(0);
-      // the first wait_dma_barrier() waits on vmcnt only: retire these LDS writes before it, so
-      // other waves' iteration-0 reads of lse/delta are ordered by that barrier (in the loop the
-      // mid-iteration lgkmcnt(0) + s_barrier does this for later tiles)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      dma_tile(0, 0, 0);
-      adv(lh, lt);
-      if (total > 1) load_ld(lh, lt);
-    }
-  } else if (total > 0) {
-    prefetch(0, 0);
-  }
-  for (int it = 0; it < total; ++it) {
-    char* cur = smem + (DMA ? (it & 1) * KC_TILE : 0);
-    if (DMA) {
-      wait_dma_barrier();  // tile it landed; every wave is past tile it-1 (its buffer is free)
-      if (it + 1 < total) {
-        write_ld((it + 1) & 1);  // before the DMA issue: the compiler's wait for lr/dr stays cheap
-        adv(pf_h, pf_t);
-        dma_tile(pf_h, pf_t, (it + 1) & 1);
-        adv(lh, lt);
-        if (it + 2 < total) load_ld(lh, lt);
-      }
-    } else {
-      __syncthreads();
-      stage_store<4>(DK ? cur : cur + C_BQ * 256, xr, tid);
-      write_ld(0);
-      __syncthreads();
-      if (++pf_t == per_head) { pf_t = 0; ++pf_h; }
-      if (it + 1 < total) prefetch(pf_h, pf_t);
-    }
-    const char* qs = cur;
-    const char* gs = cur + C_BQ * 256;
-    const float* ls = reinterpret_cast<const float*>(cur + 2 * C_BQ * 256);
-    const float* ds = ls + C_BQ;
-    const int qbase = (qt0 + cur_t) * C_BQ;
-    if (++cur_t == per_head) cur_t = 0;
-    // phase 1 (both 32-query halves): dK role dP = dO V^T, dV role S = Q K^T -> P (to LDS)
-    f32x16 c[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int q0 = qbase + 32 * kb;
-      // (no zero fill: a skipped half is skipped again in phase 2, and a dead value costs no copies)
-      if (causal && q0 + 31 < k0) continue;  // every query of the half precedes our keys
-      {  // -delta (dK role) / -lse2 (dV role) of the half's 32 query rows, in accumulator order
-        const float* rowc = (DK ? ds : ls) + 32 * kb + 4 * h;
-        const float4v r0 = *reinterpret_cast<const float4v*>(rowc), r1 = *reinterpret_cast<const float4v*>(rowc + 8),
-                      r2 = *reinterpret_cast<const float4v*>(rowc + 16), r3 = *reinterpret_cast<const float4v*>(rowc + 24);
-        c[kb] = __builtin_shufflevector(__builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7),
-                                        __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4, 5, 6,
-                                        7, 8, 9, 10, 11, 12, 13, 14, 15);
-      }
-      const char* img = DK ? gs : qs;
-      bf16x8 xa[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) xa[s] = lds_row(img, 32 * kb + c32, 2 * s + h);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {  // row operands read two k-steps ahead
-        bf16x8 xn = xa[s & 1];
-        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
-        __builtin_amdgcn_sched_barrier(0);
-        c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
-        __builtin_amdgcn_sched_barrier(0);
-        xa[s & 1] = xn;
-      }
-      if (!DK) {
-        // element r of the lane is query row q0 + 4h + ro (ro = (r&3) + 8(r>>2)), key column
-        // `key`: masked iff key > query, i.e. mthr > ro
-        const bool tile_mask = causal && q0 < k0 + 31;  // wave-uniform: only diagonal tiles pay the mask
-        if (tile_mask) {
-          asm volatile("" ::: "memory");  // keeps this a branch: merged, every tile paid the select
-          const int mthr = key - q0 - 4 * h;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float4v pv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float p = fast_exp2(c[kb][4 * g + e]);
-              pv[e] = mthr > e + 8 * g ? 0.f : p;
-              c[kb][4 * g + e] = pv[e];
-            }
-            pbuf[(kb * 4 + g) * 64 + lane] = pv;
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float4v pv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              pv[e] = fast_exp2(c[kb][4 * g + e]);
-              c[kb][4 * g + e] = pv[e];
-            }
-            pbuf[(kb * 4 + g) * 64 + lane] = pv;
-          }
-        }
-      }
-    }
-    if (DMA)  // P of every pair visible (no vmcnt wait: the next tile's DMA stays in flight)
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else
-      __syncthreads();
-    // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int q0 = qbase + 32 * kb;
-      if (causal && q0 + 31 < k0) continue;
-      if (DK) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4v pv = pbuf[(kb * 4 + g) * 64 + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = pv[e] * c[kb][4 * g + e];  // dS = P (dP - delta)
-        }
-      }
-      const bf16x8 s0 = pack8(c[kb], 0), s1 = pack8(c[kb], 8);
-      const char* op = DK ? qs : gs;  // dK^T += Q^T dS ; dV^T += dO^T P
-      bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        bf16x8 n0 = t0, n1 = t1;
-        if (d < 3) {
-          n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
-          n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc[d] = mfma(t0, s0, acc[d]);
-        acc[d] = mfma(t1, s1, acc[d]);
-        __builtin_amdgcn_sched_barrier(0);
-        t0 = n0;
-        t1 = n1;
-      }
-    }
-  }
-  if (key < S) {
-    store_row_t21(out + b * bs + (long)key * ld + (long)hk * HD, acc, DK ? scale : 1.f, h);
-  }
-}
-
-// ---------------------------------------------------- paired dK | dV kernel, one barrier per tile
-// Same roles and MFMA work as kc_body (DMA mode), rescheduled around ONE workgroup barrier per
-// 64-query tile instead of two.  The two-barrier schedule parks each role at every phase boundary
-// behind the other role's VALU (P = exp in phase 1 on the dV side, dS = P (dP - delta) in phase 2
-// on the dK side): SQ_WAIT_ANY 38 % of wave cycles, MFMA busy 36 % (profiles/r02_flash).
-//   * Q/dO tiles in a 3-deep LDS ring: tile t+1's DMA is issued right after the barrier of tile
-//     t-1, so the single barrier of tile t (vmcnt(0) + lgkmcnt(0) + s_barrier, placed between
-//     phase 1 and phase 2) both publishes P(t) and makes tile t+1 visible -- phase 1 of t+1 needs
-//     no barrier of its own;
-//   * P crosses between the pair as bf16 (the value the dV MFMA consumes anyway) through a
-//     double-buffered 4 KB-per-pair slot, because phase 1 of t+1 (writer) may overlap phase 2 of t
-//     (reader);
-//   * after barrier t: ring slot (t+2)%3 and P slot (t+1)&1 are free (their last readers ran phase
-//     2 of t-1, before phase 1 of t).
-// LDS: 3 x 33 KB tiles + 32 KB P = 130 KB (one workgroup per CU, as before).
-constexpr int KC3_PB = 4 * 4096;  // one P slot: 4 wave pairs x 4 KB (bf16)
-
-template <bool DK>
-__device__ __forceinline__ void kc3_body(const ushort* __restrict__ Q, const ushort* __restrict__ dO,
-                                         const float* __restrict__ LSE, const float* __restrict__ Dl,
-                                         const ushort* Kb, const ushort* Vb, ushort* __restrict__ out,
-                                         char* smem, int b, int hk, int kblk0, int S, int Hq, int G, long ld,
-                                         long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-  const int k0 = kblk0 + 32 * w;
-  const int key = k0 + c32;
-  const ushort* fb = DK ? Vb : Kb;
-  bf16x8 kf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-    kf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(fb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
-  f32x16 acc[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) acc[d] = f32x16(0.f);
-
-  const int nqt = (S + C_BQ - 1) / C_BQ;
-  const int qt0 = causal ? kblk0 / C_BQ : 0;
-  const int per_head = nqt - qt0;
-  const int total = G * per_head;
-  float lr = 0.f, dr = 0.f;
-  int lq = 0;
-  unsigned rc[4];
-  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto tile_at = [&](int i) { return smem + (i % 3) * KC_TILE; };
-  auto dma_tile = [&](int h_i, int t_i, int i) {
-    const int hq = hk * G + h_i;
-    const int qq0 = (qt0 + t_i) * C_BQ;
-    const ushort* base = DK ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
-    const long ldx = DK ? ld : ldo;
-    const unsigned img = lds0 + (i % 3) * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 4096;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
-      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
-    }
-  };
-  // lse / delta of one tile: raw loads into registers one tile before they are written to LDS
-  // (the write makes the compiler wait for them -- done BEFORE the next DMA issue, so that wait
-  // never covers a just-issued tile DMA it cannot see)
-  auto load_ld = [&](int h_i, int t_i) {
-    if (DK && tid < C_BQ) {
-      const int hq = hk * G + h_i;
-      lq = (qt0 + t_i) * C_BQ + tid;
-      const long st = ((long)b * Hq + hq) * S;
-      const int qc = min(lq, S - 1);
-      lr = LSE[st + qc];
-      dr = Dl[st + qc];
-    }
-  };
-  auto write_ld = [&](int i) {
-    if (DK && tid < C_BQ) {
-      float* l = reinterpret_cast<float*>(tile_at(i) + 2 * C_BQ * 256);
-      l[tid] = lq < S ? lr * LOG2E : INFINITY;  // rows past S: P = 0 exactly
-      l[C_BQ + tid] = lq < S ? dr : 0.f;
-    }
-  };
-  int dh = 0, dt = 0;  // (head, tile) of the next DMA
-  int lh = 0, lt = 0;  // (head, tile) of the lse / delta registers
-  auto adv = [&](int& hh, int& tt) {
-    if (++tt == per_head) { tt = 0; ++hh; }
-  };
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // K/V fragment loads retired (a wait the compiler sees)
-#pragma unroll
-  for (int u = 0; u < 4; ++u) rc[u] = img_rc(wu * 4096 + u * 1024 + lane * 16);
-  // prologue: tiles 0 and 1 in flight, lse / delta of tile 2 in registers
-  for (int i = 0; i < 2 && i < total; ++i) {
-    load_ld(lh, lt);
-    write_ld(i);
-    adv(lh, lt);
-    dma_tile(dh, dt, i);
-    adv(dh, dt);
-  }
-  if (total > 2) load_ld(lh, lt);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-  ushort4v* pslot = reinterpret_cast<ushort4v*>(smem + 3 * KC_TILE + w * 4096);
-  int cur_t = 0;
-  for (int it = 0; it < total; ++it) {
-    const char* cur = tile_at(it);
-    const char* qs = cur;
-    const char* gs = cur + C_BQ * 256;
-    const float* ls = reinterpret_cast<const float*>(cur + 2 * C_BQ * 256);
-    const float* ds = ls + C_BQ;
-    ushort4v* pb = pslot + (it & 1) * (KC3_PB / 8);
-    const int qbase = (qt0 + cur_t) * C_BQ;
-    if (++cur_t == per_head) cur_t = 0;
-    // phase 1: dK role dP = dO V^T, dV role S = Q K^T -> P (bf16 to the pair's P slot)
-    f32x16 c[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int q0 = qbase + 32 * kb;
-      c[kb] = f32x16(0.f);
-      if (causal && q0 + 31 < k0) continue;
-      const char* img = DK ? gs : qs;
-      bf16x8 xa[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) xa[s] = lds_row(img, 32 * kb + c32, 2 * s + h);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        bf16x8 xn = xa[s & 1];
-        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
-        __builtin_amdgcn_sched_barrier(0);
-        c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
-        __builtin_amdgcn_sched_barrier(0);
-        xa[s & 1] = xn;
-      }
-      if (!DK) {
-        const bool tile_mask = causal && q0 < k0 + 31;
-        const int mthr = tile_mask ? key - q0 - 4 * h : -0x7fffffff;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4v lv = *reinterpret_cast<const float4v*>(ls + 32 * kb + 4 * h + 8 * g);
-          ushort4v pw;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float p = fast_exp2(c[kb][4 * g + e] * scale_log2 - lv[e]);
-            const float pm = mthr > e + 8 * g ? 0.f : p;
-            pw[e] = f2bf(pm);
-            c[kb][4 * g + e] = bf2f(pw[e]);  // the dV MFMA and the dK side use the same rounded P
-          }
-          pb[(kb * 4 + g) * 64 + lane] = pw;
-        }
-      }
-    }
-    // the tile's one barrier: P(it) published; tile it+1 (DMA issued a tile ago) landed everywhere;
-    // every wave is past phase 2 of it-1, so ring slot (it+2)%3 and P slot (it+1)&1 are free
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (it + 2 < total) {
-      write_ld(it + 2);
-      adv(lh, lt);
-      dma_tile(dh, dt, it + 2);
-      adv(dh, dt);
-      if (it + 3 < total) load_ld(lh, lt);
-    }
-    // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int q0 = qbase + 32 * kb;
-      if (causal && q0 + 31 < k0) continue;
-      if (DK) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const ushort4v pw = pb[(kb * 4 + g) * 64 + lane];
-          const float4v dv4 = *reinterpret_cast<const float4v*>(ds + 32 * kb + 4 * h + 8 * g);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) c[kb][4 * g + e] = bf2f(pw[e]) * (c[kb][4 * g + e] - dv4[e]);
-        }
-      }
-      const bf16x8 s0 = pack8(c[kb], 0), s1 = pack8(c[kb], 8);
-      const char* op = DK ? qs : gs;
-      bf16x8 t0 = lds_tr(op, 32 * kb, 0, lane), t1 = lds_tr(op, 32 * kb + 16, 0, lane);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        bf16x8 n0 = t0, n1 = t1;
-        if (d < 3) {
-          n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
-          n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc[d] = mfma(t0, s0, acc[d]);
-        acc[d] = mfma(t1, s1, acc[d]);
-        __builtin_amdgcn_sched_barrier(0);
-        t0 = n0;
-        t1 = n1;
-      }
-    }
-  }
-  if (key < S) {
-    store_row_t21(out + b * bs + (long)key * ld + (long)hk * HD, acc, DK ? scale : 1.f, h);
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void fa_bwd_kc3_kernel(
-    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
-    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
-    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
-    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(1024))) char smem[3 * KC_TILE + 2 * KC3_PB];
-  const int nkb = (S + C_BK - 1) / C_BK;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int grp = L / nkb, kb_i = L % nkb;
-  const int b = grp / Hkv, hk = grp % Hkv;
-  const int kblk = causal ? kb_i : nkb - 1 - kb_i;
-  const int G = Hq / Hkv;
-  const ushort* Kb = K + b * bs + (long)hk * HD;
-  const ushort* Vb = V + b * bs + (long)hk * HD;
-  if (threadIdx.x >= 256)
-    kc3_body<false>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
-                    scale_log2, causal);
-  else
-    kc3_body<true>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
-                   scale_log2, causal);
-}
-
-template <bool DMA>
-__global__ __launch_bounds__(512, 1) void fa_bwd_kc_kernel(
-    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
-    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
-    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
-    long bs, long ldo, long bso, float scale, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(1024))) char smem[(DMA ? 2 : 1) * KC_TILE + 4 * 8192];  // tile(s) | P exchange
-  const int nkb = (S + C_BK - 1) / C_BK;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  // (batch, kv head)-major: the key blocks of one group run together on an XCD and share its
-  // Q/dO stream in L2 (key-block-major across groups measured 1.6x slower)
-  const int grp = L / nkb, kb_i = L % nkb;
-  const int b = grp / Hkv, hk = grp % Hkv;
-  const int kblk = causal ? kb_i : nkb - 1 - kb_i;
-  const int G = Hq / Hkv;
-  const ushort* Kb = K + b * bs + (long)hk * HD;
-  const ushort* Vb = V + b * bs + (long)hk * HD;
-  // wave-uniform role split; both roles pass the same barriers (same tile sequence)
-  if (threadIdx.x >= 256)
-    kc_body<false, DMA>(Q, dO, LSE, Dl, Kb, Vb, dV, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
-                   scale_log2, causal);
-  else
-    kc_body<true, DMA>(Q, dO, LSE, Dl, Kb, Vb, dK, smem, b, hk, kblk * C_BK, S, Hq, G, ld, bs, ldo, bso, scale,
-                  scale_log2, causal);
-}
+constexpr int C_BQ = 64, KC_TILE = 2 * C_BQ * 256 + 2 * C_BQ * 4;  // one staged Q|dO|lse|delta tile
 
 // ------------------------------------ paired dK | dV kernel, half width: two workgroups per CU
-// The same roles and MFMA work as kc_body (DMA mode), in workgroups of 4 waves over 64 keys: one
-// dK wave and one dV wave per 32-key slice, two slices.  The 8-wave kernel holds one workgroup per
+// The paired roles above in workgroups of 4 waves over 64 keys: one dK wave and one dV wave per
+// 32-key slice, two slices.  The retired 8-wave kernel (kc, one workgroup per CU; its code and the
+// one-barrier kc3 variant: profiles/r03_flash/retired_kc_kernels.patch) held one workgroup per
 // CU, so its 8 waves pass the same two barriers per tile together and every phase boundary
 // (barrier, first LDS operands, MFMA -> exp) is exposed on all of them at once (39.8 % MFMA busy,
 // profiles/r02_flash).  With two independent workgroups per CU the waves of one SIMD belong to
 // different barrier domains, as in the dQ kernel (60.5 % busy).  LDS per workgroup: two Q|dO
 // tiles (DMA double buffer) + the P exchange of the two pairs, as bf16 (the value the dV MFMA
 // consumes): 2 x 33 KB + 8 KB = 73 KB, two workgroups = 146 KB of the 160 KB.
-#ifndef TH_KH_EXPERIMENT
-#define TH_KH_EXPERIMENT 0  // timing probes (bit0 no P barrier, bit1 no exponentials, bit2 no LDS operand
-                            // reads after the first, bit3 no Q|dO DMA after the first tile, bit4 no wait for
-                            // the DMA at the tile barrier, bit5 contiguous DMA sources); results wrong
-#endif
-#if TH_KH_EXPERIMENT & 2
-#define KH_EXP2(x) (x)
-#else
-#define KH_EXP2(x) fast_exp2(x)
-#endif
 constexpr int KH_BK = 64, KH_LDS = 2 * KC_TILE + 2 * 4096;
 
 template <bool DK>
@@ -1389,12 +895,8 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
     const unsigned img = lds0 + buf * KC_TILE + (DK ? 0 : C_BQ * 256) + wu * 8192;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-#if TH_KH_EXPERIMENT & 32  // timing probe: each piece reads 1 KB of contiguous bytes from the tile's first row on
-      glds16(base, (unsigned)(min(qq0, S - 1) * ldx) * 2u + (unsigned)(u * 1024 + lane * 16), img + u * 1024);
-#else
       const int row = min(qq0 + (int)(rc[u] & 255), S - 1);
       glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
-#endif
     }
   };
   float lr = 0.f, dr = 0.f;
@@ -1433,15 +935,11 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
   }
   for (int it = 0; it < total; ++it) {
     char* cur = smem + (it & 1) * KC_TILE;
-#if TH_KH_EXPERIMENT & 16  // timing probe: the tile barrier without waiting for the DMA
-    asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
-#else
     wait_dma_barrier();  // tile it landed; every wave is past tile it-1 (its buffer is free)
-#endif
     if (it + 1 < total) {
       write_ld((it + 1) & 1);
       adv(pf_h, pf_t);
-      if (!(TH_KH_EXPERIMENT & 8)) dma_tile(pf_h, pf_t, (it + 1) & 1);
+      dma_tile(pf_h, pf_t, (it + 1) & 1);
       adv(lh, lt);
       if (it + 2 < total) load_ld(lh, lt);
     }
@@ -1472,7 +970,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         bf16x8 xn = xa[s & 1];
-        if (!(TH_KH_EXPERIMENT & 4) && s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
+        if (s + 2 < 8) xn = lds_row(img, 32 * kb + c32, 2 * s + 4 + h);
         __builtin_amdgcn_sched_barrier(0);
         c[kb] = mfma(xa[s & 1], kf[s], c[kb]);
         fill(s);
@@ -1498,12 +996,12 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
       init_c(1);
       chain1(0, no_fill);
       chain1(1, [&](int s) {
-        c[0][2 * s] = KH_EXP2(c[0][2 * s]);
-        c[0][2 * s + 1] = KH_EXP2(c[0][2 * s + 1]);
+        c[0][2 * s] = fast_exp2(c[0][2 * s]);
+        c[0][2 * s + 1] = fast_exp2(c[0][2 * s + 1]);
       });
       publish_p(0);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) c[1][r] = KH_EXP2(c[1][r]);
+      for (int r = 0; r < 16; ++r) c[1][r] = fast_exp2(c[1][r]);
       publish_p(1);
     } else {
 #pragma unroll
@@ -1519,22 +1017,18 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
             const int mthr = key - q0 - 4 * h;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const float p = KH_EXP2(c[kb][r]);
+              const float p = fast_exp2(c[kb][r]);
               c[kb][r] = mthr > (r & 3) + 8 * (r >> 2) ? 0.f : p;
             }
           } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) c[kb][r] = KH_EXP2(c[kb][r]);
+            for (int r = 0; r < 16; ++r) c[kb][r] = fast_exp2(c[kb][r]);
           }
           publish_p(kb);
         }
       }
     }
-#if TH_KH_EXPERIMENT & 1  // timing probe only (wrong results): no P-exchange barrier
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // P of both pairs visible
-#endif
     // phase 2: dK role dS = P (dP - delta), dK^T += Q^T dS; dV role dV^T += dO^T P
     const char* op = DK ? qs : gs;
     auto chain2 = [&](int kb, const bf16x8& s0, const bf16x8& s1, auto&& fill) {
@@ -1543,7 +1037,7 @@ __device__ __forceinline__ void kh_body(const ushort* __restrict__ Q, const usho
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         bf16x8 n0 = t0, n1 = t1;
-        if (!(TH_KH_EXPERIMENT & 4) && d < 3) {
+        if (d < 3) {
           n0 = lds_tr(op, 32 * kb, 32 * d + 32, lane);
           n1 = lds_tr(op, 32 * kb + 16, 32 * d + 32, lane);
         }
@@ -1665,7 +1159,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
                           int Hkv, int D, int causal, long ld, long bs, long ldo, long bso, float scale,
                           const float* rcos, const float* rsin, int flags, hipStream_t s) {
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
-  if (rcos != nullptr && ((flags & (8 | 32 | 64 | 128 | 256)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
+  if (rcos != nullptr && ((flags & (8 | 32)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
     return -3;
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
@@ -1683,32 +1177,14 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     if (dq_dma) TH_DQ_LAUNCH(true, true); else TH_DQ_LAUNCH(true, false);
   }
 #undef TH_DQ_LAUNCH
-  // flags bit3: the fused dK/dV kernel (default: the paired key-centric kernels below)
-  if (!(flags & 8)) {
-    const long nkc = (long)((S + C_BK - 1) / C_BK) * Hkv * B;
-    // default: the half-width paired kernel (two workgroups per CU; step -0.4 % against the 8-wave
-    // one, profiles/r03_flash); bit8: the 8-wave paired kernel (round-2 default); bit7: its
-    // one-barrier variant; bit6 (or bit5 / 32-bit offset overflow): register-staged Q/dO tiles
-    if (dq_dma && !(flags & (256 | 128 | 64))) {
-      const long nkh = (long)((S + KH_BK - 1) / KH_BK) * Hkv * B;
-      fa_bwd_kh_kernel<<<(unsigned)nkh, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                     (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
-                                                     B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal,
-                                                     rcos, rsin);
-    } else if (dq_dma && (flags & 128))  // bit7: one barrier per tile (3-deep Q/dO ring, bf16 P exchange)
-      fa_bwd_kc3_kernel<<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                      (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
-                                                      B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal);
-    else if (dq_dma && !(flags & 64))  // same 32-bit offset bound; bit5 or bit6: register staging here
-      fa_bwd_kc_kernel<true><<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                           (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
-                                                           B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
-                                                           causal);
-    else
-      fa_bwd_kc_kernel<false><<<(unsigned)nkc, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
-                                                            (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
-                                                            B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E,
-                                                            causal);
+  // default: the half-width paired dK|dV kernel (two workgroups per CU, profiles/r03_flash); flags
+  // bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused register-staged dK/dV kernel below
+  if (!(flags & 8) && dq_dma) {
+    const long nkh = (long)((S + KH_BK - 1) / KH_BK) * Hkv * B;
+    fa_bwd_kh_kernel<<<(unsigned)nkh, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                   (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,
+                                                   B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal,
+                                                   rcos, rsin);
     TH_CHECK_LAUNCH();
   }
   const long nk = (long)((S + B_BK - 1) / B_BK) * Hkv * B;

@@ -3,75 +3,149 @@
 //
 //     C[M][N] (+)= sum_k A[M][k] * B[N][k]        (y = x W^T;  dX = dY (W^T)^T on a W^T copy)
 //
-// Same machine as the TN weight-gradient kernel (gemm_tn.hip, ping-pong v2), with the operand
-// path of the K-contiguous layout:
-//   * tile 256 x 256, k-tiles of 32 in a 4-stage LDS ring (4 x 32 KB); 8 waves as 2 (M) x 4 (N),
-//     wave tile 128 x 64, v_mfma_f32_32x32x16_bf16, 128 f32 accumulators per lane;
-//   * LDS-DMA (global_load_lds_dwordx4, inline asm, scalar base + one constant lane offset) stages
-//     16 rows x 64 B per wave-instruction; 16-B chunk c of row r lands in slot c ^ ((r >> 2) & 3),
-//     applied on the global source because the DMA writes lane-linearly;
-//   * an MFMA operand is ONE ds_read_b128 of a row (8 consecutive k), conflict-free under that
-//     swizzle: a 16-lane group reads 16 rows = (r & 3) 64-B quarters x ((r >> 2) & 3) slots;
-//   * ping-pong wave groups (G0 = waves 0-3, rows 0-127; G1 = waves 4-7, rows 128-255): one group
-//     gathers its fragments of k-tile t and issues its operand's DMA two k-tiles ahead while the
-//     other runs its 16 MFMAs, one barrier per slot, counted vmcnt (never 0 in the loop);
+// One wave per SIMD, the machine hipBLASLt's MT256x256x64_MI16x16 kernel is (profiles/r03_gemm:
+// 83.7 % MFMA busy, one wave per SIMD), with the register allocation taken away from the compiler:
+//   * workgroup tile 256 x 256, k-tiles of 64, 4 waves as 2 (M) x 2 (N), wave tile 128 x 128 =
+//     8 x 8 blocks of v_mfma_f32_16x16x32_bf16 -> 64 f32x4 accumulators = all 256 AGPRs.  Every
+//     MFMA is an inline-asm statement whose accumulator operand is "+a": the accumulators live in
+//     the accumulator file for the whole kernel and hipcc has nothing to shuffle (round 3's HIP
+//     version of this machine spent 3.2x hipBLASLt's VALU on v_accvgpr moves and ran 0.58-0.67x);
+//   * A and B images of a k-tile (256 rows x 128 B each) are staged by LDS-DMA
+//     (global_load_lds_dwordx4) into a 2-stage ring (128 KB); 16-B chunk c of image row r lands in
+//     slot c ^ ((r >> 1) & 7), applied on the global source because the DMA writes lane-linearly.
+//     An MFMA operand is ONE ds_read_b128 (16 rows x 4 chunks); under this swizzle a 16-lane group
+//     hits 16 distinct 16-B slots of the bank row: conflict-free;
+//   * each k-tile is two phases of 64 MFMAs (k 0-31, k 32-63).  Phase A computes half 0 while it
+//     reads half 1's 16 fragments; one barrier (after this wave's DMA of the next tile retired)
+//     makes the next tile visible; phase B computes half 1 while it reads the NEXT tile's half 0
+//     and issues this wave's 16 DMA pieces of the tile after that into the stage just freed.  So
+//     fragments are always one phase ahead, DMA one tile ahead, one barrier per k-tile, and the
+//     LDS reads / DMA issues sit in the MFMA shadow (one read per 4 MFMAs);
+//   * the MFMA runs with the operands swapped (B block as "A"), so a lane holds 4 consecutive
+//     columns of one output row; the epilogue goes through LDS (per wave, no barrier) and leaves
+//     as 16-B row stores;
 //   * XCD-aware grouped tile order (bands of 8 tile rows per XCD).
+// Round 3's ping-pong NT kernel (2 waves per SIMD, 0.77-0.86x hipBLASLt) is in git history.
 #include "th_common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
 namespace {
-constexpr int TM = 256, TN = 256, TK = 32;
-constexpr int NTHR = 512;
-constexpr int ROWB = TK * 2;         // 64 B per staged row
-constexpr int OPB = TM * ROWB;       // 16 KB per operand image
-constexpr int STAGEB = 2 * OPB;      // A + B
-constexpr int NSTAGE = 4;
+constexpr int BM = 256, BN = 256, BK = 64, NTHR = 256;
+constexpr int IMG = BM * BK * 2;   // 32 KB per operand image
+constexpr int STAGE = 2 * IMG;     // A | B
+constexpr int SMEM = 2 * STAGE;    // 128 KB
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// one LDS-DMA piece: 64 lanes x 16 B from (sbase + voff) into LDS [lds, lds + 1 KB)
 __device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
                :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
 }
 
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+// acc (accumulator file) += a . b
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ bf16x8 lds_rd(const char LDS_AS* p) { return *reinterpret_cast<const bf16x8 LDS_AS*>(p); }
+
+// fragment read order of a phase: the next phase starts with block row 0 (A0 against B0..B7)
+__device__ constexpr int RD_ORDER[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};  // <8: A, else B
+
+struct Ctx {
+  const char LDS_AS* smem;
+  unsigned lds0;
+  int rd[2];          // lane's fragment byte offset in an image row block, per k-half
+  int a_wave, b_wave;  // wave's row block offset inside the A / B image
+  // DMA: scalar bases of this wave's first A / B piece at k = 0, lane offsets per piece parity
+  const ushort* ga;
+  const ushort* gb;
+  long lda, ldb;
+  unsigned va[2], vb[2];
+  int dma_row;  // first image row this wave stages
+};
+
+// 16 DMA pieces (8 of A, 8 of B) of k-tile `kt` into stage `st`; piece p issued at step p
+template <int P>
+__device__ __forceinline__ void dma_piece(const Ctx& c, int kt, int st) {
+  const unsigned img = c.lds0 + st * STAGE + (P < 8 ? 0 : IMG) + (c.dma_row + (P & 7) * 8) * 128;
+  if (P < 8)
+    glds16(c.ga + (long)(P & 7) * 8 * c.lda + kt * BK, c.va[P & 1], img);
+  else
+    glds16(c.gb + (long)(P & 7) * 8 * c.ldb + kt * BK, c.vb[P & 1], img);
 }
 
-__device__ __forceinline__ bf16x8 lds_b128(const char LDS_AS* p) { return *reinterpret_cast<const bf16x8 LDS_AS*>(p); }
-
-// Rows [row0, row0+256) x k [k0, k0+32) of a row-major [rows][ld] operand into one 16 KB image:
-// 16 wave-instructions of 16 rows, 4 per wave of the staging group.  `loff` = the lane's constant
-// byte offset (row (lane>>2), swizzled chunk) from the instruction's scalar base.
-__device__ __forceinline__ void stage_nt(const ushort* __restrict__ g, unsigned loff, long ld, long row0, long k0,
-                                         unsigned img, int w4) {
+// One phase: acc[i][j] += B_j(.) A_i over the k-half held in (af, bf) -- 64 MFMAs in 16 groups of
+// 4, i-major -- with the 16 fragment reads of the next half into (an, bn) from stage `rst` /
+// k-half `rk` two per group in groups 0-7 (RD), and this wave's 16 DMA pieces of k-tile `dkt` into
+// stage `dst` two per group in groups 8-15 (DMA).
+template <bool RD, bool DMA>
+__device__ __forceinline__ void phase(const Ctx& c, f32x4 (&acc)[8][8], const bf16x8 (&af)[8], const bf16x8 (&bf)[8],
+                                      bf16x8 (&an)[8], bf16x8 (&bn)[8], int rst, int rk, int dkt, int dst) {
+  const char LDS_AS* sa = c.smem + rst * STAGE + c.a_wave + c.rd[rk];
+  const char LDS_AS* sb = c.smem + rst * STAGE + IMG + c.b_wave + c.rd[rk];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int u = i * 4 + w4;
-    glds16(g + (row0 + 16 * u) * ld + k0, loff, img + u * 1024);
+  for (int s = 0; s < 16; ++s) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = 4 * s + q, i = m >> 3, j = m & 7;
+      mfma_acc(acc[i][j], bf[j], af[i]);
+    }
+    // fragment reads in the first half of the phase (two per group): hipcc waits lgkmcnt(0) at the
+    // loop head, so the last read must be long retired by the end of phase B
+    if (RD && s < 8) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int f = RD_ORDER[2 * s + e];
+        if (f < 8)
+          an[f] = lds_rd(sa + f * 2048);
+        else
+          bn[f - 8] = lds_rd(sb + (f - 8) * 2048);
+      }
+    }
+    // DMA pieces in the second half (two per group), behind the reads
+    if (DMA && s >= 8) {
+      switch (s) {  // constant after unrolling
+        case 8: dma_piece<0>(c, dkt, dst); dma_piece<8>(c, dkt, dst); break;
+        case 9: dma_piece<1>(c, dkt, dst); dma_piece<9>(c, dkt, dst); break;
+        case 10: dma_piece<2>(c, dkt, dst); dma_piece<10>(c, dkt, dst); break;
+        case 11: dma_piece<3>(c, dkt, dst); dma_piece<11>(c, dkt, dst); break;
+        case 12: dma_piece<4>(c, dkt, dst); dma_piece<12>(c, dkt, dst); break;
+        case 13: dma_piece<5>(c, dkt, dst); dma_piece<13>(c, dkt, dst); break;
+        case 14: dma_piece<6>(c, dkt, dst); dma_piece<14>(c, dkt, dst); break;
+        default: dma_piece<7>(c, dkt, dst); dma_piece<15>(c, dkt, dst); break;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-__device__ __forceinline__ unsigned lane_off_nt(long ld, int lane) {
-  const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
-  return (unsigned)(2 * ((long)(lane >> 2) * ld + 8 * chunk));
+// this wave's 16 DMA pieces of k-tile kt into stage st, back to back (prologue)
+__device__ __forceinline__ void dma_tile(const Ctx& c, int kt, int st) {
+  dma_piece<0>(c, kt, st); dma_piece<1>(c, kt, st); dma_piece<2>(c, kt, st); dma_piece<3>(c, kt, st);
+  dma_piece<4>(c, kt, st); dma_piece<5>(c, kt, st); dma_piece<6>(c, kt, st); dma_piece<7>(c, kt, st);
+  dma_piece<8>(c, kt, st); dma_piece<9>(c, kt, st); dma_piece<10>(c, kt, st); dma_piece<11>(c, kt, st);
+  dma_piece<12>(c, kt, st); dma_piece<13>(c, kt, st); dma_piece<14>(c, kt, st); dma_piece<15>(c, kt, st);
 }
 
-// vmcnt(4 * n), n in 0..1 (immediate operand)
-__device__ __forceinline__ void wait_dma_barrier(int n) {
-  if (n >= 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+__device__ __forceinline__ void read_half(const Ctx& c, bf16x8 (&af)[8], bf16x8 (&bf)[8], int st, int k) {
+  const char LDS_AS* sa = c.smem + st * STAGE + c.a_wave + c.rd[k];
+  const char LDS_AS* sb = c.smem + st * STAGE + IMG + c.b_wave + c.rd[k];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int f = RD_ORDER[s];
+    if (f < 8)
+      af[f] = lds_rd(sa + f * 2048);
+    else
+      bf[f - 8] = lds_rd(sb + (f - 8) * 2048);
+  }
 }
 }  // namespace
 
@@ -79,12 +153,10 @@ template <bool BETA>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restrict__ A, long lda,
                                                          const ushort* __restrict__ B, long ldb,
                                                          ushort* __restrict__ C, long ldc, int M, int N, int K) {
-  constexpr int AHEAD = 2;
-  __shared__ __attribute__((aligned(1024))) char smem_raw[NSTAGE * STAGEB];
-  char LDS_AS* smem = (char LDS_AS*)smem_raw;
-  const int nM = M / TM, nN = N / TN;
+  __shared__ __attribute__((aligned(1024))) char smem_raw[SMEM];
+  const int nM = M / BM, nN = N / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 8;
+  constexpr int GM = 8;  // a band of 8 tile rows walks the tile columns together (A rows stay in L2)
   const int per_band = GM * nN;
   const int band = L / per_band;
   const int first_m = band * GM;
@@ -92,397 +164,125 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
   const int in_band = L % per_band;
   const int tm = first_m + in_band % gm;
   const int tn = in_band / gm;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
 
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 2, wn = w & 3, w4 = w & 3;
-  const bool g1 = w >= 4;
-  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
-  const int nt = K / TK;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int r16 = lane & 15, g = lane >> 4;
 
-  const int i32 = lane & 31, h = lane >> 5;
-  int ch[2];
+  Ctx c;
+  c.smem = (const char LDS_AS*)smem_raw;
+  c.lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem_raw;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) ch[ks] = ((2 * ks + h) ^ ((i32 >> 2) & 3)) * 16;
-  int a_row[4], b_row[2];
+  for (int k = 0; k < 2; ++k) c.rd[k] = r16 * 128 + (((4 * k + g) ^ (r16 >> 1)) << 4);
+  c.a_wave = wr * 128 * 128;
+  c.b_wave = wc * 128 * 128;
+  c.dma_row = w * 64;  // wave w stages image rows [64 w, 64 w + 64) of A and of B
+  c.lda = lda;
+  c.ldb = ldb;
+  c.ga = A + (m0 + c.dma_row) * lda;
+  c.gb = B + (n0 + c.dma_row) * ldb;
+  {
+    // piece p covers image rows dma_row + 8p .. +7; lane -> row (lane >> 3), slot (lane & 7), which
+    // holds global chunk slot ^ ((row >> 1) & 7) = slot ^ (4 (p & 1) + (lane >> 4))
+    const int rr = lane >> 3, slot = lane & 7;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) a_row[mb] = (wm * 128 + 32 * mb + i32) * ROWB;
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb) b_row[nb] = (wn * 64 + 32 * nb + i32) * ROWB;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16(0.f);
-
-  const unsigned lds0 = (unsigned)(uintptr_t)smem;
-  const unsigned la = lane_off_nt(lda, lane), lb = lane_off_nt(ldb, lane);
-#pragma unroll
-  for (int j = 0; j < AHEAD; ++j) {
-    if (j < nt) {
-      if (!g1) stage_nt(A, la, lda, m0, (long)j * TK, lds0 + j * STAGEB, w4);
-      else stage_nt(B, lb, ldb, n0, (long)j * TK, lds0 + j * STAGEB + OPB, w4);
+    for (int par = 0; par < 2; ++par) {
+      const int chunk = slot ^ (4 * par + (lane >> 4));
+      c.va[par] = (unsigned)(2 * ((long)rr * lda + 8 * chunk));
+      c.vb[par] = (unsigned)(2 * ((long)rr * ldb + 8 * chunk));
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  if (g1) asm volatile("s_barrier" ::: "memory");  // G1 enters one slot late
 
-  bf16x8 af[4][2], bf[2][2];
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.f);
+
+  const int nt = K / BK;
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  dma_tile(c, 0, 0);
+  if (nt > 1) {
+    dma_tile(c, 1, 1);
+    asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  read_half(c, a0, b0, 0, 0);
+
+  // One straight-line body for every k-tile: a branch between MFMA statements would give the
+  // accumulators phi nodes on several paths, and hipcc then copies them through VGPRs (and spills).
+  // So the last two tiles' phase B runs the same code: it re-stages the last k-tile into the free
+  // stage (nobody reads it) and reads fragments nobody uses.
   for (int t = 0; t < nt; ++t) {
-    const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
-    // ---- gather slot (+ this group's operand DMA two k-tiles ahead)
-    if (t + AHEAD < nt) {
-      const unsigned st = lds0 + ((t + AHEAD) & (NSTAGE - 1)) * STAGEB;
-      if (!g1) stage_nt(A, la, lda, m0, (long)(t + AHEAD) * TK, st, w4);
-      else stage_nt(B, lb, ldb, n0, (long)(t + AHEAD) * TK, st + OPB, w4);
-    }
-    const char LDS_AS* sa = smem + (t & (NSTAGE - 1)) * STAGEB;
-    const char LDS_AS* sb = sa + OPB;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb) af[mb][ks] = lds_b128(sa + a_row[mb] + ch[ks]);
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) bf[nb][ks] = lds_b128(sb + b_row[nb] + ch[ks]);
-    }
-    if (g1) {  // G1's B image of k-tile t+1 lands before G0 gathers it (next slot)
-      wait_dma_barrier(younger);
-    } else {
-      asm volatile("s_barrier" ::: "memory");
-    }
-    // ---- compute slot
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = mfma(af[mb][ks], bf[nb][ks], acc[mb][nb]);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!g1) {  // G0's A image of k-tile t+1 landed before the barrier that opens its gather
-      wait_dma_barrier(younger);
-    } else {
-      asm volatile("s_barrier" ::: "memory");
-    }
+    const int st = t & 1;
+    // phase A: half 0 of tile t; read half 1 of tile t
+    phase<true, false>(c, acc, a0, b0, a1, b1, st, 1, 0, 0);
+    // this wave's DMA of tile t+1 retired, every wave's fragment reads of stage st done -> tile t+1
+    // visible to all, stage st free for tile t+2
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // phase B: half 1 of tile t; read half 0 of tile t+1; DMA tile t+2 into stage st
+    phase<true, true>(c, acc, a1, b1, a0, b0, st ^ 1, 0, min(t + 2, nt - 1), st);
   }
-  if (!g1) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last re-staged pieces
+  // MFMA results -> readable (XDL write -> VALU read wait states), then pin every accumulator
+  // after the pad so no read of it is scheduled above
+  asm volatile("s_nop 15\n\ts_nop 15" ::);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
 
+  // epilogue: lane holds C[m = 16 i + r16][n = 16 j + 4 g .. +3] of the wave tile.  Stage the wave's
+  // 128 x 128 bf16 tile in its own 32 KB of LDS (rows of 256 B, 16-B block b of row r at b ^ (r & 15):
+  // conflict-free b64 writes and b128 reads), then 16-B row stores.  The last phase still read and
+  // DMA'd stage images, so every wave must be past it first.
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  char LDS_AS* ep = (char LDS_AS*)smem_raw + w * 32768;
+  const long crow0 = m0 + wr * 128, ccol0 = n0 + wc * 128;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const long n = n0 + wn * 64 + 32 * nb + i32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long m = m0 + wm * 128 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float v = acc[mb][nb][r];
-        if (BETA) v += bf2f(C[m * ldc + n]);
-        C[m * ldc + n] = f2bf(v);
-      }
-    }
-}
-
-// The same kernel on v_mfma_f32_16x16x32_bf16 (hipBLASLt's MFMA shape on gfx950): one k-step per
-// 32-deep k-tile, wave tile 128 x 64 = 8 x 4 blocks of 16 x 16 (f32x4 accumulators), operand of
-// lane l = row (l & 15), k chunk (l >> 4): still one ds_read_b128, conflict-free under the same
-// swizzle.  Guide: bare 16x16x32 loops hold a higher clock under load than 32x32x16 at equal
-// cycles per FLOP (MI355X_MICROARCH 'DVFS give-back' item 7).
-template <bool BETA>
-__global__ __launch_bounds__(NTHR, 1) void gemm_nt16_kernel(const ushort* __restrict__ A, long lda,
-                                                           const ushort* __restrict__ B, long ldb,
-                                                           ushort* __restrict__ C, long ldc, int M, int N, int K) {
-  constexpr int AHEAD = 2;
-  __shared__ __attribute__((aligned(1024))) char smem_raw[NSTAGE * STAGEB];
-  char LDS_AS* smem = (char LDS_AS*)smem_raw;
-  const int nM = M / TM, nN = N / TN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 8;
-  const int per_band = GM * nN;
-  const int band = L / per_band;
-  const int first_m = band * GM;
-  const int gm = min(GM, nM - first_m);
-  const int in_band = L % per_band;
-  const int tm = first_m + in_band % gm;
-  const int tn = in_band / gm;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 2, wn = w & 3, w4 = w & 3;
-  const bool g1 = w >= 4;
-  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
-  const int nt = K / TK;
-
-  const int i16 = lane & 15, kg = lane >> 4;
-  const int chk = (kg ^ ((i16 >> 2) & 3)) * 16;
-  int a_row[8], b_row[4];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb) a_row[mb] = (wm * 128 + 16 * mb + i16) * ROWB + chk;
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) b_row[nb] = (wn * 64 + 16 * nb + i16) * ROWB + chk;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4(0.f);
-
-  const unsigned lds0 = (unsigned)(uintptr_t)smem;
-  const unsigned la = lane_off_nt(lda, lane), lb = lane_off_nt(ldb, lane);
-#pragma unroll
-  for (int j = 0; j < AHEAD; ++j) {
-    if (j < nt) {
-      if (!g1) stage_nt(A, la, lda, m0, (long)j * TK, lds0 + j * STAGEB, w4);
-      else stage_nt(B, lb, ldb, n0, (long)j * TK, lds0 + j * STAGEB + OPB, w4);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  if (g1) asm volatile("s_barrier" ::: "memory");
-
-  bf16x8 af[8], bf[4];
-  for (int t = 0; t < nt; ++t) {
-    const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
-    if (t + AHEAD < nt) {
-      const unsigned st = lds0 + ((t + AHEAD) & (NSTAGE - 1)) * STAGEB;
-      if (!g1) stage_nt(A, la, lda, m0, (long)(t + AHEAD) * TK, st, w4);
-      else stage_nt(B, lb, ldb, n0, (long)(t + AHEAD) * TK, st + OPB, w4);
-    }
-    const char LDS_AS* sa = smem + (t & (NSTAGE - 1)) * STAGEB;
-    const char LDS_AS* sb = sa + OPB;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb) af[mb] = lds_b128(sa + a_row[mb]);
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) bf[nb] = lds_b128(sb + b_row[nb]);
-    if (g1) {
-      wait_dma_barrier(younger);
-    } else {
-      asm volatile("s_barrier" ::: "memory");
-    }
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma16(af[mb], bf[nb], acc[mb][nb]);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!g1) {
-      wait_dma_barrier(younger);
-    } else {
-      asm volatile("s_barrier" ::: "memory");
-    }
-  }
-  if (!g1) asm volatile("s_barrier" ::: "memory");
-
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const long n = n0 + wn * 64 + 16 * nb + i16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long m = m0 + wm * 128 + 16 * mb + 4 * kg + r;
-        float v = acc[mb][nb][r];
-        if (BETA) v += bf2f(C[m * ldc + n]);
-        C[m * ldc + n] = f2bf(v);
-      }
-    }
-}
-
-// Variants of the 16x16x32 kernel for the round-3 hipBLASLt-parity probe (profiles/r03_gemm):
-//   * AHEAD / NS: DMA depth.  AHEAD 3 with a 5-stage ring (the whole 160 KB LDS) gives every
-//     k-tile's LDS-DMA three k-tiles (six slots) to land instead of two;
-//   * PRIO: s_setprio 1 around each wave's MFMA block (the guide's T5 static form);
-//   * LDSEPI: the output tile leaves through LDS as whole rows -- each lane stores 16 B (8 columns)
-//     per instruction instead of 2-B scalars at a 64-row stride (guide T21 / "O staged through
-//     LDS"): the f32 accumulators of one group's 64-row half are written to a padded [64][260] f32
-//     image (row stride 1040 B: the 4 row groups of a wave land 16 banks apart), then all 512
-//     threads read 8 consecutive columns each and store them (C += in f32 when BETA), 4 rounds.
-template <bool BETA, int AHEAD, int NS, bool PRIO, bool LDSEPI>
-__global__ __launch_bounds__(NTHR, 1) void gemm_nt16v_kernel(const ushort* __restrict__ A, long lda,
-                                                            const ushort* __restrict__ B, long ldb,
-                                                            ushort* __restrict__ C, long ldc, int M, int N, int K) {
-  __shared__ __attribute__((aligned(1024))) char smem_raw[NS * STAGEB];
-  char LDS_AS* smem = (char LDS_AS*)smem_raw;
-  const int nM = M / TM, nN = N / TN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 8;
-  const int per_band = GM * nN;
-  const int band = L / per_band;
-  const int first_m = band * GM;
-  const int gm = min(GM, nM - first_m);
-  const int in_band = L % per_band;
-  const int tm = first_m + in_band % gm;
-  const int tn = in_band / gm;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 2, wn = w & 3, w4 = w & 3;
-  const bool g1 = w >= 4;
-  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
-  const int nt = K / TK;
-
-  const int i16 = lane & 15, kg = lane >> 4;
-  const int chk = (kg ^ ((i16 >> 2) & 3)) * 16;
-  int a_row[8], b_row[4];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb) a_row[mb] = (wm * 128 + 16 * mb + i16) * ROWB + chk;
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) b_row[nb] = (wn * 64 + 16 * nb + i16) * ROWB + chk;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4(0.f);
-
-  const unsigned lds0 = (unsigned)(uintptr_t)smem;
-  const unsigned la = lane_off_nt(lda, lane), lb = lane_off_nt(ldb, lane);
-#pragma unroll
-  for (int j = 0; j < AHEAD; ++j) {
-    if (j < nt) {
-      if (!g1) stage_nt(A, la, lda, m0, (long)j * TK, lds0 + j * STAGEB, w4);
-      else stage_nt(B, lb, ldb, n0, (long)j * TK, lds0 + j * STAGEB + OPB, w4);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  if (g1) asm volatile("s_barrier" ::: "memory");
-
-  int cur = 0, nxt = AHEAD % NS;  // ring slots of k-tile t and of k-tile t + AHEAD
-  bf16x8 af[8], bf[4];
-  for (int t = 0; t < nt; ++t) {
-    const int younger = min(AHEAD - 1, max(0, nt - 1 - (t + 1)));
-    if (t + AHEAD < nt) {
-      const unsigned st = lds0 + nxt * STAGEB;
-      if (!g1) stage_nt(A, la, lda, m0, (long)(t + AHEAD) * TK, st, w4);
-      else stage_nt(B, lb, ldb, n0, (long)(t + AHEAD) * TK, st + OPB, w4);
-    }
-    const char LDS_AS* sa = smem + cur * STAGEB;
-    const char LDS_AS* sb = sa + OPB;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb) af[mb] = lds_b128(sa + a_row[mb]);
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) bf[nb] = lds_b128(sb + b_row[nb]);
-    auto wait_barrier = [&]() {
-      if (AHEAD >= 3 && younger >= 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else if (younger >= 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    if (g1) wait_barrier();
-    else asm volatile("s_barrier" ::: "memory");
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma16(af[mb], bf[nb], acc[mb][nb]);
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (!g1) wait_barrier();
-    else asm volatile("s_barrier" ::: "memory");
-    cur = cur + 1 == NS ? 0 : cur + 1;
-    nxt = nxt + 1 == NS ? 0 : nxt + 1;
-  }
-  if (!g1) asm volatile("s_barrier" ::: "memory");
-
-  if (!LDSEPI) {
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const long n = n0 + wn * 64 + 16 * nb + i16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const long m = m0 + wm * 128 + 16 * mb + 4 * kg + r;
-          float v = acc[mb][nb][r];
-          if (BETA) v += bf2f(C[m * ldc + n]);
-          C[m * ldc + n] = f2bf(v);
-        }
-      }
-    return;
-  }
-  // ---- epilogue through LDS: 4 rounds of 64 output rows (group g, half h of its 128 rows)
-  constexpr int EROW = 260;  // f32 per padded image row
-  float LDS_AS* img = (float LDS_AS*)smem;
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done with the ring
-#pragma unroll
-  for (int round = 0; round < 4; ++round) {
-    const int g = round >> 1, h = round & 1;
-    if ((int)g1 == g) {
-#pragma unroll
-      for (int mbh = 0; mbh < 4; ++mbh)
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * mbh + 4 * kg + r, col = wn * 64 + 16 * nb + i16;
-            img[row * EROW + col] = acc[4 * h + mbh][nb][r];
-          }
-    }
-    __syncthreads();
-    // 64 rows x 32 chunks of 8 columns = 2048 chunks over 512 threads
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = tid + q * NTHR, row = c >> 5, col8 = (c & 31) * 8;
-      const float LDS_AS* src = img + row * EROW + col8;
-      const float4v lo = *reinterpret_cast<const float4v LDS_AS*>(src);
-      const float4v hi = *reinterpret_cast<const float4v LDS_AS*>(src + 4);
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      ushort* dst = C + (m0 + g * 128 + h * 64 + row) * ldc + n0 + col8;
+    for (int j = 0; j < 8; ++j) {
+      f32x4 v = acc[i][j];
       if (BETA) {
-        const ushort8 old = *reinterpret_cast<const ushort8*>(dst);
+        const ushort4v old = *reinterpret_cast<const ushort4v*>(C + (crow0 + 16 * i + r16) * ldc + ccol0 + 16 * j + 4 * g);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += bf2f(old[j]);
+        for (int e = 0; e < 4; ++e) v[e] += bf2f(old[e]);
       }
-      ushort8 o;
+      ushort4v o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-      *reinterpret_cast<ushort8*>(dst) = o;
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      const int row = 16 * i + r16;
+      const int blk = (2 * j + (g >> 1)) ^ r16;
+      *reinterpret_cast<ushort4v LDS_AS*>(ep + row * 256 + blk * 16 + (g & 1) * 8) = o;
     }
-    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const int row = 4 * q + g;
+    const ushort8 v = *reinterpret_cast<const ushort8 LDS_AS*>(ep + row * 256 + ((r16 ^ (row & 15)) << 4));
+    *reinterpret_cast<ushort8*>(C + (crow0 + row) * ldc + ccol0 + 8 * r16) = v;
   }
 }
 
-template <bool BETA>
-static void launch_nt16v(int variant, unsigned grid, hipStream_t s, const ushort* A, long lda, const ushort* B,
-                         long ldb, ushort* C, long ldc, int M, int N, int K) {
-  // variant bits: 1 = deep ring (AHEAD 3, 5 stages), 2 = setprio, 4 = LDS epilogue
-  switch (variant & 7) {
-#define TH_NT16V(V, AH, NSS, PR, LE)                                                                            \
-  case V:                                                                                                     \
-    gemm_nt16v_kernel<BETA, AH, NSS, PR, LE><<<grid, NTHR, 0, s>>>(A, lda, B, ldb, C, ldc, M, N, K);          \
-    break;
-    TH_NT16V(0, 2, 4, false, false)
-    TH_NT16V(1, 3, 5, false, false)
-    TH_NT16V(2, 2, 4, true, false)
-    TH_NT16V(3, 3, 5, true, false)
-    TH_NT16V(4, 2, 4, false, true)
-    TH_NT16V(5, 3, 5, false, true)
-    TH_NT16V(6, 2, 4, true, true)
-    TH_NT16V(7, 3, 5, true, true)
-#undef TH_NT16V
-  }
-}
-
-// C[M][N] (+)= A[M][K] B[N][K]^T (row strides lda, ldb, ldc in elements).  -1: shape not tiled.
 extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                           int beta, int flags, hipStream_t s) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK) return -1;
+  (void)flags;
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -1;
-  // the lane offset and the per-instruction scalar bases stay within 32-bit byte offsets per row block
-  if ((long)16 * lda * 2 >= (1L << 31) || (long)16 * ldb * 2 >= (1L << 31)) return -1;
-  const unsigned grid = (unsigned)((long)(M / TM) * (N / TN));
-  if (flags & 14) {  // round-3 variants of the 16x16x32 kernel: flags bits 1-3 = variant bits 0-2
-    const int v = (flags >> 1) & 7;
-    if (beta)
-      launch_nt16v<true>(v, grid, s, (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
-    else
-      launch_nt16v<false>(v, grid, s, (const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
-    TH_CHECK_LAUNCH();
-  }
-  if (flags & 1) {  // 16x16x32 MFMA variant
-    if (beta)
-      gemm_nt16_kernel<true><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
-    else
-      gemm_nt16_kernel<false><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
-    TH_CHECK_LAUNCH();
-  }
+  // per-lane DMA offsets are 32-bit: 8 rows of one piece from the piece's scalar base
+  if ((long)8 * lda * 2 >= (1L << 31) || (long)8 * ldb * 2 >= (1L << 31)) return -1;
+  const long grid = (long)(M / BM) * (N / BN);
+  if (grid > 0x7fffffffL) return -2;
   if (beta)
-    gemm_nt_kernel<true><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
+    gemm_nt_kernel<true><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C,
+                                                         ldc, M, N, K);
   else
-    gemm_nt_kernel<false><<<grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K);
+    gemm_nt_kernel<false><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C,
+                                                          ldc, M, N, K);
   TH_CHECK_LAUNCH();
 }

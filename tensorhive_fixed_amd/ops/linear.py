@@ -27,6 +27,7 @@ import os
 import torch
 
 from ._grad import deliver, mm_into
+from .gemm_nt import nt_into, nt_mm
 from .gemm_tn import gemm_tn_, supported as _tn_supported
 from .transpose import transpose
 
@@ -56,7 +57,7 @@ class _Linear(torch.autograd.Function):
         if residual is not None:
             y = torch.addmm(residual.reshape(-1, w.shape[0]), x2, w.t())
         else:
-            y = torch.mm(x2, w.t())
+            y = nt_mm(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.has_res = residual is not None
         ctx.xshape = x.shape
@@ -69,7 +70,7 @@ class _Linear(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
         if dy2.is_cuda and _DGRAD_NT:
-            dx = torch.mm(dy2, transpose(w).t())
+            dx = nt_mm(dy2, transpose(w))
         else:
             dx = torch.mm(dy2, w)
         dx = dx.view(ctx.xshape)
@@ -78,7 +79,7 @@ class _Linear(torch.autograd.Function):
             gw = deliver(w, tn_into(dyc, xc), lambda: torch.mm(dyc.t(), xc))
         elif ctx.wgrad_nt and dy2.is_cuda and _WGRAD_NT:
             dyT, xT = transpose(_c(dy2)), transpose(_c(x2))
-            gw = deliver(w, mm_into(dyT, xT.t()), lambda: torch.mm(dyT, xT.t()))
+            gw = deliver(w, nt_into(dyT, xT), lambda: torch.mm(dyT, xT.t()))
         else:
             gw = deliver(w, mm_into(dy2.t(), x2), lambda: torch.mm(dy2.t(), x2))
         return dx, gw, (dy if ctx.has_res else None), None, None

@@ -18,6 +18,7 @@ import torch
 
 from . import _lib
 from ._grad import deliver, mm_into
+from .gemm_nt import nt_into, nt_mm
 from .linear import _DGRAD_NT, linear
 from .swiglu import swiglu, swiglu_reference
 from .transpose import transpose
@@ -29,7 +30,7 @@ class _GateUpSwiGLU(torch.autograd.Function):
         h2 = h.reshape(-1, h.shape[-1])
         if not h2.is_contiguous():
             h2 = h2.contiguous()
-        gu = torch.mm(h2, w13.t())
+        gu = nt_mm(h2, w13) if h2.is_cuda else torch.mm(h2, w13.t())
         T, F2 = gu.shape
         F = F2 // 2
         if gu.is_cuda:
@@ -54,10 +55,10 @@ class _GateUpSwiGLU(torch.autograd.Function):
             dguT = torch.empty((F2, T), device=gu.device, dtype=gu.dtype)
             _lib.call("th_swiglu_bwd_t", d2.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, F,
                       _lib.stream_ptr(gu.device))
-            dh = torch.mm(dgu, transpose(w13).t()) if _DGRAD_NT else torch.mm(dgu, w13)
+            dh = nt_mm(dgu, transpose(w13)) if _DGRAD_NT else torch.mm(dgu, w13)
             del dgu
             hT = transpose(h2)
-            gw = deliver(w13, mm_into(dguT, hT.t()), lambda: torch.mm(dguT, hT.t()))
+            gw = deliver(w13, nt_into(dguT, hT), lambda: torch.mm(dguT, hT.t()))
         else:
             g, u = gu.float().chunk(2, dim=-1)
             s = torch.sigmoid(g)
