@@ -291,7 +291,7 @@ class AmdMonitorConfig:
     probe_enabled: bool
     probe_period: float
     stub_gpus: int
-    counters_enabled: bool = False
+    counters_enabled: bool = True
     counters_period_ms: int = 1000
     # tasks count their own HBM bytes (libthhbm via ROCP_TOOL_LIBRARIES, core/hbm.py)
     task_hbm_counters: bool = True
@@ -472,7 +472,7 @@ def load_config(directory: Path | str | None = None) -> Config:
             probe_enabled=main.bool("amd_monitor", "probe_enabled", True),
             probe_period=main.float("amd_monitor", "probe_period", 1.0),
             stub_gpus=main.int("amd_monitor", "stub_gpus", 8),
-            counters_enabled=main.bool("amd_monitor", "counters_enabled", False),
+            counters_enabled=main.bool("amd_monitor", "counters_enabled", True),
             counters_period_ms=main.int("amd_monitor", "counters_period_ms", 1000),
             task_hbm_counters=main.bool("amd_monitor", "task_hbm_counters", True),
             remote_mode=main.str("amd_monitor", "remote_mode", "agent"),
