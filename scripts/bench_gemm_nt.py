@@ -5,6 +5,7 @@ operands (median of 15 launches per arm, 3 rounds, best round).  One JSON line p
     python scripts/bench_gemm_nt.py [SHAPE ...]
 """
 import json
+import os
 import statistics
 import sys
 
@@ -18,6 +19,9 @@ T, D, F, V = 32768, 4096, 14336, 128256
 SHAPES = [("wqkv.fwd", T, 6144, D), ("wo.fwd", T, D, D), ("w13.fwd", T, 2 * F, D), ("w2.fwd", T, D, F),
           ("wqkv.dgrad", T, D, 6144), ("wo.dgrad", T, D, D), ("w13.dgrad", T, D, 2 * F), ("w2.dgrad", T, F, D),
           ("w13.wgrad", 2 * F, D, T), ("head.fwd", 4096, V, D), ("head.dgrad", 4096, D, V)]
+
+
+VARIANTS = [int(v) for v in os.environ.get("GEMM_VARIANTS", "0").split(",")]
 
 
 def timed(fn, iters=15):
@@ -57,15 +61,19 @@ def main():
         gemm_nt_(a, b, c)
         torch.mm(a, b.t(), out=c2)
         diff = ((c.float() - c2.float()).norm() / c2.float().norm()).item()
-        res = {"nt": [], "hipblaslt": []}
+        res = {f"v{v}": [] for v in VARIANTS}
+        res["hipblaslt"] = []
         for _ in range(3):
-            res["nt"].append(timed(lambda: gemm_nt_(a, b, c)))
+            for v in VARIANTS:
+                res[f"v{v}"].append(timed(lambda: gemm_nt_(a, b, c, variant=v)))
             res["hipblaslt"].append(timed(lambda: torch.mm(a, b.t(), out=c2)))
         fl = 2.0 * M * N * K
-        nt, hb = min(res["nt"]), min(res["hipblaslt"])
-        print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "nt_ms": round(nt, 4), "hipblaslt_ms": round(hb, 4),
-                          "nt_tflops": round(fl / nt / 1e9), "hipblaslt_tflops": round(fl / hb / 1e9),
-                          "speedup": round(hb / nt, 3), "rel_diff_vs_hipblaslt": diff}), flush=True)
+        hb = min(res["hipblaslt"])
+        tf = {k: round(fl / min(v) / 1e9) for k, v in res.items()}
+        best = max((k for k in tf if k != "hipblaslt"), key=lambda k: tf[k])
+        print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "tflops": tf, "best": best,
+                          "best_vs_hipblaslt": round(tf[best] / tf["hipblaslt"], 3), "hipblaslt_ms": round(hb, 4),
+                          "rel_diff_vs_hipblaslt": diff}), flush=True)
         del a, b, c, c2
     return 0
 

@@ -44,9 +44,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // one LDS-DMA piece: 64 lanes x 16 B from (sbase + voff) into LDS [lds, lds + 1 KB)
+template <bool NOP>
 __device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-               :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
+  if (NOP)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                 :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                 :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
 }
 
 // acc (accumulator file) += a . b
@@ -72,25 +77,30 @@ struct Ctx {
   int dma_row;  // first image row this wave stages
 };
 
-// 16 DMA pieces (8 of A, 8 of B) of k-tile `kt` into stage `st`; piece p issued at step p
-template <int P>
+// One of the 16 DMA pieces (8 of A, 8 of B) of k-tile `kt` into stage `st`.  The piece's scalar base
+// is loop-invariant (hipcc keeps the 16 of them in SGPR pairs); the k-tile offset rides in the
+// lane's 32-bit offset (one v_add per operand and parity per tile instead of a 64-bit SALU add per
+// piece).
+template <int P, int V>
 __device__ __forceinline__ void dma_piece(const Ctx& c, int kt, int st) {
   const unsigned img = c.lds0 + st * STAGE + (P < 8 ? 0 : IMG) + (c.dma_row + (P & 7) * 8) * 128;
+  const unsigned koff = (unsigned)kt * (BK * 2);
   if (P < 8)
-    glds16(c.ga + (long)(P & 7) * 8 * c.lda + kt * BK, c.va[P & 1], img);
+    glds16<!(V & 2)>(c.ga + (long)(P & 7) * 8 * c.lda, c.va[P & 1] + koff, img);
   else
-    glds16(c.gb + (long)(P & 7) * 8 * c.ldb + kt * BK, c.vb[P & 1], img);
+    glds16<!(V & 2)>(c.gb + (long)(P & 7) * 8 * c.ldb, c.vb[P & 1] + koff, img);
 }
 
 // One phase: acc[i][j] += B_j(.) A_i over the k-half held in (af, bf) -- 64 MFMAs in 16 groups of
-// 4, i-major -- with the 16 fragment reads of the next half into (an, bn) from stage `rst` /
-// k-half `rk` two per group in groups 0-7 (RD), and this wave's 16 DMA pieces of k-tile `dkt` into
-// stage `dst` two per group in groups 8-15 (DMA).
-template <bool RD, bool DMA>
+// 4, i-major.  RD0 >= 0: the 16 fragment reads of the next half into (an, bn) from stage `rst` /
+// k-half `rk`, spread over groups RD0 .. RD0+RDN-1 (RDN 8: two per group, 16: one).  DMA0 >= 0:
+// this wave's 16 DMA pieces of k-tile `dkt` into stage `dst`, over groups DMA0 .. DMA0+DMAN-1.
+template <int RD0, int RDN, int DMA0, int DMAN, int V>
 __device__ __forceinline__ void phase(const Ctx& c, f32x4 (&acc)[8][8], const bf16x8 (&af)[8], const bf16x8 (&bf)[8],
                                       bf16x8 (&an)[8], bf16x8 (&bn)[8], int rst, int rk, int dkt, int dst) {
   const char LDS_AS* sa = c.smem + rst * STAGE + c.a_wave + c.rd[rk];
   const char LDS_AS* sb = c.smem + rst * STAGE + IMG + c.b_wave + c.rd[rk];
+  constexpr int RPG = RDN > 0 ? 16 / RDN : 0, DPG = DMAN > 0 ? 16 / DMAN : 0;
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
 #pragma unroll
@@ -98,29 +108,91 @@ __device__ __forceinline__ void phase(const Ctx& c, f32x4 (&acc)[8][8], const bf
       const int m = 4 * s + q, i = m >> 3, j = m & 7;
       mfma_acc(acc[i][j], bf[j], af[i]);
     }
-    // fragment reads in the first half of the phase (two per group): hipcc waits lgkmcnt(0) at the
-    // loop head, so the last read must be long retired by the end of phase B
-    if (RD && s < 8) {
+    if (RD0 >= 0 && s >= RD0 && s < RD0 + RDN) {
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int f = RD_ORDER[2 * s + e];
+      for (int e = 0; e < RPG; ++e) {
+        const int f = RD_ORDER[RPG * (s - RD0) + e];
         if (f < 8)
           an[f] = lds_rd(sa + f * 2048);
         else
           bn[f - 8] = lds_rd(sb + (f - 8) * 2048);
       }
     }
-    // DMA pieces in the second half (two per group), behind the reads
-    if (DMA && s >= 8) {
-      switch (s) {  // constant after unrolling
-        case 8: dma_piece<0>(c, dkt, dst); dma_piece<8>(c, dkt, dst); break;
-        case 9: dma_piece<1>(c, dkt, dst); dma_piece<9>(c, dkt, dst); break;
-        case 10: dma_piece<2>(c, dkt, dst); dma_piece<10>(c, dkt, dst); break;
-        case 11: dma_piece<3>(c, dkt, dst); dma_piece<11>(c, dkt, dst); break;
-        case 12: dma_piece<4>(c, dkt, dst); dma_piece<12>(c, dkt, dst); break;
-        case 13: dma_piece<5>(c, dkt, dst); dma_piece<13>(c, dkt, dst); break;
-        case 14: dma_piece<6>(c, dkt, dst); dma_piece<14>(c, dkt, dst); break;
-        default: dma_piece<7>(c, dkt, dst); dma_piece<15>(c, dkt, dst); break;
+    if (DMA0 >= 0 && s >= DMA0 && s < DMA0 + DMAN) {
+#pragma unroll
+      for (int e = 0; e < DPG; ++e) {
+        const int u = DPG * (s - DMA0) + e;  // A0 B0 A1 B1 ... (piece u>>1 of A or B)
+        switch (u) {  // constant after unrolling
+          case 0: dma_piece<0, V>(c, dkt, dst); break;
+          case 1: dma_piece<8, V>(c, dkt, dst); break;
+          case 2: dma_piece<1, V>(c, dkt, dst); break;
+          case 3: dma_piece<9, V>(c, dkt, dst); break;
+          case 4: dma_piece<2, V>(c, dkt, dst); break;
+          case 5: dma_piece<10, V>(c, dkt, dst); break;
+          case 6: dma_piece<3, V>(c, dkt, dst); break;
+          case 7: dma_piece<11, V>(c, dkt, dst); break;
+          case 8: dma_piece<4, V>(c, dkt, dst); break;
+          case 9: dma_piece<12, V>(c, dkt, dst); break;
+          case 10: dma_piece<5, V>(c, dkt, dst); break;
+          case 11: dma_piece<13, V>(c, dkt, dst); break;
+          case 12: dma_piece<6, V>(c, dkt, dst); break;
+          case 13: dma_piece<14, V>(c, dkt, dst); break;
+          case 14: dma_piece<7, V>(c, dkt, dst); break;
+          default: dma_piece<15, V>(c, dkt, dst); break;
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Fine-grained form of `phase` (variant bit 3): the side work is interleaved per MFMA instead of per
+// group of 4, so no burst of DMA / read issue outlasts the issue slots an MFMA leaves free (one
+// wave per SIMD: an MFMA holds vector issue for 8 of its 16 cycles).  With DMA (phase B): a DMA
+// piece after MFMAs 0, 4, .., 60 and a fragment read after MFMAs 2, 6, .., 62; without (phase A):
+// a read after MFMAs 0, 3, .., 45.
+template <bool RD, bool DMA, int V>
+__device__ __forceinline__ void phase_fine(const Ctx& c, f32x4 (&acc)[8][8], const bf16x8 (&af)[8],
+                                           const bf16x8 (&bf)[8], bf16x8 (&an)[8], bf16x8 (&bn)[8], int rst, int rk,
+                                           int dkt, int dst) {
+  const char LDS_AS* sa = c.smem + rst * STAGE + c.a_wave + c.rd[rk];
+  const char LDS_AS* sb = c.smem + rst * STAGE + IMG + c.b_wave + c.rd[rk];
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    const int i = m >> 3, j = m & 7;
+    mfma_acc(acc[i][j], bf[j], af[i]);
+    int r = -1, d = -1;
+    if (DMA) {
+      if ((m & 3) == 0) d = m >> 2;
+      if (RD && (m & 3) == 2) r = m >> 2;
+    } else if (RD && m % 3 == 0 && m / 3 < 16) {
+      r = m / 3;
+    }
+    if (r >= 0) {
+      const int f = RD_ORDER[r];
+      if (f < 8)
+        an[f] = lds_rd(sa + f * 2048);
+      else
+        bn[f - 8] = lds_rd(sb + (f - 8) * 2048);
+    }
+    if (d >= 0) {
+      switch (d) {  // A0 B0 A1 B1 ...; constant after unrolling
+        case 0: dma_piece<0, V>(c, dkt, dst); break;
+        case 1: dma_piece<8, V>(c, dkt, dst); break;
+        case 2: dma_piece<1, V>(c, dkt, dst); break;
+        case 3: dma_piece<9, V>(c, dkt, dst); break;
+        case 4: dma_piece<2, V>(c, dkt, dst); break;
+        case 5: dma_piece<10, V>(c, dkt, dst); break;
+        case 6: dma_piece<3, V>(c, dkt, dst); break;
+        case 7: dma_piece<11, V>(c, dkt, dst); break;
+        case 8: dma_piece<4, V>(c, dkt, dst); break;
+        case 9: dma_piece<12, V>(c, dkt, dst); break;
+        case 10: dma_piece<5, V>(c, dkt, dst); break;
+        case 11: dma_piece<13, V>(c, dkt, dst); break;
+        case 12: dma_piece<6, V>(c, dkt, dst); break;
+        case 13: dma_piece<14, V>(c, dkt, dst); break;
+        case 14: dma_piece<7, V>(c, dkt, dst); break;
+        default: dma_piece<15, V>(c, dkt, dst); break;
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -128,11 +200,12 @@ __device__ __forceinline__ void phase(const Ctx& c, f32x4 (&acc)[8][8], const bf
 }
 
 // this wave's 16 DMA pieces of k-tile kt into stage st, back to back (prologue)
+template <int V>
 __device__ __forceinline__ void dma_tile(const Ctx& c, int kt, int st) {
-  dma_piece<0>(c, kt, st); dma_piece<1>(c, kt, st); dma_piece<2>(c, kt, st); dma_piece<3>(c, kt, st);
-  dma_piece<4>(c, kt, st); dma_piece<5>(c, kt, st); dma_piece<6>(c, kt, st); dma_piece<7>(c, kt, st);
-  dma_piece<8>(c, kt, st); dma_piece<9>(c, kt, st); dma_piece<10>(c, kt, st); dma_piece<11>(c, kt, st);
-  dma_piece<12>(c, kt, st); dma_piece<13>(c, kt, st); dma_piece<14>(c, kt, st); dma_piece<15>(c, kt, st);
+  dma_piece<0, V>(c, kt, st); dma_piece<1, V>(c, kt, st); dma_piece<2, V>(c, kt, st); dma_piece<3, V>(c, kt, st);
+  dma_piece<4, V>(c, kt, st); dma_piece<5, V>(c, kt, st); dma_piece<6, V>(c, kt, st); dma_piece<7, V>(c, kt, st);
+  dma_piece<8, V>(c, kt, st); dma_piece<9, V>(c, kt, st); dma_piece<10, V>(c, kt, st); dma_piece<11, V>(c, kt, st);
+  dma_piece<12, V>(c, kt, st); dma_piece<13, V>(c, kt, st); dma_piece<14, V>(c, kt, st); dma_piece<15, V>(c, kt, st);
 }
 
 __device__ __forceinline__ void read_half(const Ctx& c, bf16x8 (&af)[8], bf16x8 (&bf)[8], int st, int k) {
@@ -149,14 +222,18 @@ __device__ __forceinline__ void read_half(const Ctx& c, bf16x8 (&af)[8], bf16x8 
 }
 }  // namespace
 
-template <bool BETA>
+// V (schedule variants, A/B aids): bit0 reads and DMA one per group over all 16 groups (default:
+// two per group, reads in one half of the phase, DMA in the other); bit1 no s_nop between the M0
+// write and the LDS-DMA; bit2 bands of 16 tile rows instead of 8; bit3 side work interleaved per
+// MFMA (phase_fine).  Compiled: 0, 1, 3, 8, 10, 12.
+template <bool BETA, int V>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restrict__ A, long lda,
                                                          const ushort* __restrict__ B, long ldb,
                                                          ushort* __restrict__ C, long ldc, int M, int N, int K) {
   __shared__ __attribute__((aligned(1024))) char smem_raw[SMEM];
   const int nM = M / BM, nN = N / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GM = 8;  // a band of 8 tile rows walks the tile columns together (A rows stay in L2)
+  constexpr int GM = (V & 4) ? 16 : 8;  // a band of tile rows walks the tile columns together (A rows stay in L2)
   const int per_band = GM * nN;
   const int band = L / per_band;
   const int first_m = band * GM;
@@ -203,30 +280,46 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
 
   const int nt = K / BK;
   bf16x8 a0[8], b0[8], a1[8], b1[8];
-  dma_tile(c, 0, 0);
+  dma_tile<V>(c, 0, 0);
   if (nt > 1) {
-    dma_tile(c, 1, 1);
+    dma_tile<V>(c, 1, 1);
     asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
   read_half(c, a0, b0, 0, 0);
-
-  // One straight-line body for every k-tile: a branch between MFMA statements would give the
-  // accumulators phi nodes on several paths, and hipcc then copies them through VGPRs (and spills).
-  // So the last two tiles' phase B runs the same code: it re-stages the last k-tile into the free
-  // stage (nobody reads it) and reads fragments nobody uses.
-  for (int t = 0; t < nt; ++t) {
+  // phase A(0): half 0 of tile 0, read half 1 of tile 0
+  constexpr int RN = (V & 1) ? 16 : 8;
+  if (V & 8)
+    phase_fine<true, false, V>(c, acc, a0, b0, a1, b1, 0, 1, 0, 0);
+  else
+    phase<0, RN, -1, 0, V>(c, acc, a0, b0, a1, b1, 0, 1, 0, 0);
+  // this wave's DMA of tile 1 retired and every wave's reads of stage 0 done: tile 1 visible, and
+  // the next DMA may overwrite stage 0
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // Steady state, one loop iteration = phase B(t) + phase A(t+1) + the barrier, so the loop head sits
+  // right after a barrier (hipcc waits lgkmcnt(0) there: nothing is outstanding).  The body is
+  // straight-line -- a branch between MFMA statements would give the accumulators phi nodes on
+  // several paths, and hipcc then copies them through VGPRs and spills -- so the second-to-last
+  // B phase re-stages the last k-tile into the free stage (nobody reads it).
+  //   B(t):   half 1 of tile t; DMA tile t+2 -> stage t&1 (groups 0-7, ~2 phases before it is waited
+  //           for); read half 0 of tile t+1 (groups 8-15)
+  //   A(t+1): half 0 of tile t+1; read half 1 of tile t+1 (groups 0-7)
+  for (int t = 0; t < nt - 1; ++t) {
     const int st = t & 1;
-    // phase A: half 0 of tile t; read half 1 of tile t
-    phase<true, false>(c, acc, a0, b0, a1, b1, st, 1, 0, 0);
-    // this wave's DMA of tile t+1 retired, every wave's fragment reads of stage st done -> tile t+1
-    // visible to all, stage st free for tile t+2
+    if (V & 8) {
+      phase_fine<true, true, V>(c, acc, a1, b1, a0, b0, st ^ 1, 0, min(t + 2, nt - 1), st);
+      phase_fine<true, false, V>(c, acc, a0, b0, a1, b1, st ^ 1, 1, 0, 0);
+    } else {
+      if (V & 1)
+        phase<0, 16, 0, 16, V>(c, acc, a1, b1, a0, b0, st ^ 1, 0, min(t + 2, nt - 1), st);
+      else
+        phase<8, 8, 0, 8, V>(c, acc, a1, b1, a0, b0, st ^ 1, 0, min(t + 2, nt - 1), st);
+      phase<0, RN, -1, 0, V>(c, acc, a0, b0, a1, b1, st ^ 1, 1, 0, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // phase B: half 1 of tile t; read half 0 of tile t+1; DMA tile t+2 into stage st
-    phase<true, true>(c, acc, a1, b1, a0, b0, st ^ 1, 0, min(t + 2, nt - 1), st);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last re-staged pieces
+  phase<-1, 0, -1, 0, V>(c, acc, a1, b1, a0, b0, 0, 0, 0, 0);  // B(nt-1)
   // MFMA results -> readable (XDL write -> VALU read wait states), then pin every accumulator
   // after the pad so no read of it is scheduled above
   asm volatile("s_nop 15\n\ts_nop 15" ::);
@@ -237,9 +330,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
 
   // epilogue: lane holds C[m = 16 i + r16][n = 16 j + 4 g .. +3] of the wave tile.  Stage the wave's
   // 128 x 128 bf16 tile in its own 32 KB of LDS (rows of 256 B, 16-B block b of row r at b ^ (r & 15):
-  // conflict-free b64 writes and b128 reads), then 16-B row stores.  The last phase still read and
-  // DMA'd stage images, so every wave must be past it first.
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // conflict-free b64 writes and b128 reads), then 16-B row stores.  The last B phase reads and
+  // DMAs nothing and the barrier before it drained every wave's reads and DMA: no further barrier.
   char LDS_AS* ep = (char LDS_AS*)smem_raw + w * 32768;
   const long crow0 = m0 + wr * 128, ccol0 = n0 + wc * 128;
 #pragma unroll
@@ -270,7 +362,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
 
 extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                           int beta, int flags, hipStream_t s) {
-  (void)flags;
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -1;
@@ -278,11 +369,19 @@ extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   if ((long)8 * lda * 2 >= (1L << 31) || (long)8 * ldb * 2 >= (1L << 31)) return -1;
   const long grid = (long)(M / BM) * (N / BN);
   if (grid > 0x7fffffffL) return -2;
-  if (beta)
-    gemm_nt_kernel<true><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C,
-                                                         ldc, M, N, K);
-  else
-    gemm_nt_kernel<false><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C,
-                                                          ldc, M, N, K);
+#define TH_NT_LAUNCH(BT, V)                                                                                 \
+  gemm_nt_kernel<BT, V><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, \
+                                                       M, N, K)
+  // flags bits 0-3: schedule variant (see gemm_nt_kernel); beta = 1 runs the default schedule
+  switch (beta ? 16 : (flags & 15)) {
+    case 1: TH_NT_LAUNCH(false, 1); break;
+    case 3: TH_NT_LAUNCH(false, 3); break;
+    case 8: TH_NT_LAUNCH(false, 8); break;
+    case 10: TH_NT_LAUNCH(false, 10); break;
+    case 12: TH_NT_LAUNCH(false, 12); break;
+    case 16: TH_NT_LAUNCH(true, 0); break;
+    default: TH_NT_LAUNCH(false, 0); break;
+  }
+#undef TH_NT_LAUNCH
   TH_CHECK_LAUNCH();
 }

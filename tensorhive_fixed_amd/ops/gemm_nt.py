@@ -31,8 +31,13 @@ def usable(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> bool:
             and 16 * max(a.stride(0), b.stride(0)) < (1 << 31))
 
 
-def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
-    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation)."""
+_VARIANT = int(os.environ.get("TH_GEMM_NT_VARIANT", "0"))
+
+
+def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+             variant: int | None = None) -> torch.Tensor:
+    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation).  ``variant`` (0, 1, 3,
+    8, 10, 12; beta 0 only): schedule variants of ``csrc/gemm_nt.hip`` for A/B runs."""
     M, K = a.shape
     N, K2 = b.shape
     if K2 != K or tuple(out.shape) != (M, N):
@@ -44,7 +49,7 @@ def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
             torch.mm(a, b.t(), out=out)
         return out
     _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), 0, _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), _VARIANT if variant is None else int(variant) & 15, _lib.stream_ptr(a.device))
     return out
 
 
