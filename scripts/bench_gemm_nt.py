@@ -67,13 +67,18 @@ def main():
             for v in VARIANTS:
                 res[f"v{v}"].append(timed(lambda: gemm_nt_(a, b, c, variant=v)))
             res["hipblaslt"].append(timed(lambda: torch.mm(a, b.t(), out=c2)))
+        vdiff = {}
+        for v in VARIANTS:  # every variant's output against hipBLASLt's (same operands)
+            c.zero_()
+            gemm_nt_(a, b, c, variant=v)
+            vdiff[f"v{v}"] = ((c.float() - c2.float()).norm() / c2.float().norm()).item()
         fl = 2.0 * M * N * K
         hb = min(res["hipblaslt"])
         tf = {k: round(fl / min(v) / 1e9) for k, v in res.items()}
         best = max((k for k in tf if k != "hipblaslt"), key=lambda k: tf[k])
         print(json.dumps({"gemm": name, "M": M, "N": N, "K": K, "tflops": tf, "best": best,
                           "best_vs_hipblaslt": round(tf[best] / tf["hipblaslt"], 3), "hipblaslt_ms": round(hb, 4),
-                          "rel_diff_vs_hipblaslt": diff}), flush=True)
+                          "rel_diff_vs_hipblaslt": diff, "variant_rel_diff": vdiff}), flush=True)
         del a, b, c, c2
     return 0
 

@@ -65,6 +65,11 @@ __device__ __forceinline__ bf16x8 lds_rd(const char LDS_AS* p) { return *reinter
 __device__ constexpr int RD_ORDER[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};  // <8: A, else B
 
 struct Ctx {
+  // buffer DMA (variant bit 4): one descriptor per operand (this wave's first staged row), a
+  // loop-invariant 32-bit lane offset per piece, the k-tile offset as soffset
+  __amdgpu_buffer_rsrc_t ra, rb;
+  unsigned vpa[8], vpb[8];
+  unsigned lds_wave;  // LDS byte address of this wave's first staged A row in stage 0
   const char LDS_AS* smem;
   unsigned lds0;
   int rd[2];          // lane's fragment byte offset in an image row block, per k-half
@@ -81,8 +86,24 @@ struct Ctx {
 // is loop-invariant (hipcc keeps the 16 of them in SGPR pairs); the k-tile offset rides in the
 // lane's 32-bit offset (one v_add per operand and parity per tile instead of a 64-bit SALU add per
 // piece).
+// buffer form: s_add_u32 writes M0 directly (no VGPR or 64-bit address arithmetic per piece)
+template <int IMM>
+__device__ __forceinline__ void bdma16(unsigned lds_base, unsigned voff, __amdgpu_buffer_rsrc_t r, unsigned soff) {
+  asm volatile("s_add_u32 m0, %0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds"
+               :: "s"(lds_base), "i"(IMM), "v"(voff), "s"(r), "s"(soff) : "memory", "m0");
+}
+
 template <int P, int V>
 __device__ __forceinline__ void dma_piece(const Ctx& c, int kt, int st) {
+  if (V & 16) {
+    const unsigned lb = c.lds_wave + st * STAGE;  // uniform; the piece's constant part is an immediate
+    const unsigned soff = (unsigned)kt * (BK * 2);
+    if (P < 8)
+      bdma16<(P & 7) * 1024>(lb, c.vpa[P & 7], c.ra, soff);
+    else
+      bdma16<IMG + (P & 7) * 1024>(lb, c.vpb[P & 7], c.rb, soff);
+    return;
+  }
   const unsigned img = c.lds0 + st * STAGE + (P < 8 ? 0 : IMG) + (c.dma_row + (P & 7) * 8) * 128;
   const unsigned koff = (unsigned)kt * (BK * 2);
   if (P < 8)
@@ -225,7 +246,9 @@ __device__ __forceinline__ void read_half(const Ctx& c, bf16x8 (&af)[8], bf16x8 
 // V (schedule variants, A/B aids): bit0 reads and DMA one per group over all 16 groups (default:
 // two per group, reads in one half of the phase, DMA in the other); bit1 no s_nop between the M0
 // write and the LDS-DMA; bit2 bands of 16 tile rows instead of 8; bit3 side work interleaved per
-// MFMA (phase_fine).  Compiled: 0, 1, 3, 8, 10, 12.
+// MFMA (phase_fine); bit4 the DMA as buffer_load ... lds with a loop-invariant lane offset per piece,
+// the k offset in soffset and M0 written by one s_add (no per-piece VGPR or 64-bit address math).
+// Compiled: 0, 1, 8, 16, 17, 20 (8 + 16 loses the AGPR allocation: hipcc moves the accumulators).
 template <bool BETA, int V>
 __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restrict__ A, long lda,
                                                          const ushort* __restrict__ B, long ldb,
@@ -269,6 +292,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
       const int chunk = slot ^ (4 * par + (lane >> 4));
       c.va[par] = (unsigned)(2 * ((long)rr * lda + 8 * chunk));
       c.vb[par] = (unsigned)(2 * ((long)rr * ldb + 8 * chunk));
+    }
+    if (V & 16) {
+      c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)c.ga, 0, 0x7fffffff, 0x00020000);
+      c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)c.gb, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        c.vpa[p] = c.va[p & 1] + (unsigned)(2L * 8 * p * lda);
+        c.vpb[p] = c.vb[p & 1] + (unsigned)(2L * 8 * p * ldb);
+      }
+      c.lds_wave = c.lds0 + c.dma_row * 128;
     }
   }
 
@@ -372,14 +405,14 @@ extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void
 #define TH_NT_LAUNCH(BT, V)                                                                                 \
   gemm_nt_kernel<BT, V><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, \
                                                        M, N, K)
-  // flags bits 0-3: schedule variant (see gemm_nt_kernel); beta = 1 runs the default schedule
-  switch (beta ? 16 : (flags & 15)) {
+  // flags bits 0-4: schedule variant (see gemm_nt_kernel); beta = 1 runs the default schedule
+  switch (beta ? 64 : (flags & 31)) {
     case 1: TH_NT_LAUNCH(false, 1); break;
-    case 3: TH_NT_LAUNCH(false, 3); break;
     case 8: TH_NT_LAUNCH(false, 8); break;
-    case 10: TH_NT_LAUNCH(false, 10); break;
-    case 12: TH_NT_LAUNCH(false, 12); break;
-    case 16: TH_NT_LAUNCH(true, 0); break;
+    case 16: TH_NT_LAUNCH(false, 16); break;
+    case 17: TH_NT_LAUNCH(false, 17); break;
+    case 20: TH_NT_LAUNCH(false, 20); break;
+    case 64: TH_NT_LAUNCH(true, 0); break;
     default: TH_NT_LAUNCH(false, 0); break;
   }
 #undef TH_NT_LAUNCH

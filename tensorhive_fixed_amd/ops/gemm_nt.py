@@ -31,13 +31,14 @@ def usable(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> bool:
             and 16 * max(a.stride(0), b.stride(0)) < (1 << 31))
 
 
-_VARIANT = int(os.environ.get("TH_GEMM_NT_VARIANT", "0"))
+# schedule variant 8 (side work interleaved per MFMA) measured best on every shape (profiles/r04_gemm)
+_VARIANT = int(os.environ.get("TH_GEMM_NT_VARIANT", "8"))
 
 
 def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
              variant: int | None = None) -> torch.Tensor:
-    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation).  ``variant`` (0, 1, 3,
-    8, 10, 12; beta 0 only): schedule variants of ``csrc/gemm_nt.hip`` for A/B runs."""
+    """``out[M, N] (+)= a[M, K] @ b[N, K]ᵀ`` (bf16 in / out, f32 accumulation).  ``variant`` (0, 1, 8,
+    16, 17, 20; beta 0 only): schedule variants of ``csrc/gemm_nt.hip`` for A/B runs."""
     M, K = a.shape
     N, K2 = b.shape
     if K2 != K or tuple(out.shape) != (M, N):
@@ -49,7 +50,7 @@ def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
             torch.mm(a, b.t(), out=out)
         return out
     _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), _VARIANT if variant is None else int(variant) & 15, _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), _VARIANT if variant is None else int(variant) & 31, _lib.stream_ptr(a.device))
     return out
 
 
