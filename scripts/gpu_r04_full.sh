@@ -1,0 +1,11 @@
+# round 4: full GPU suite on the current tree, smoke, 20-step bench, step profile (kernel stats)
+R=$GRAFT_REPO_ROOT; cd $R; source scripts/gpu_step.sh; T=${FULL_TAG:-full}; mkdir -p gpurun_out/r04/$T
+run_step r04/$T/pytest 1100 python -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread
+tail -n 4 gpurun_out/r04/$T/pytest.log
+run_step r04/$T/smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+tail -n 1 gpurun_out/r04/$T/smoke.log
+run_step r04/$T/bench_20 600 python bench.py --gpus 1 --steps 20 --warmup 5
+grep metric gpurun_out/r04/$T/bench_20.log | cut -c1-260
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r04/$T/prof -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --daemon-bench 0 > $R/gpurun_out/r04/$T/prof.log 2>&1 || exit 1
+cd $R && python3 scripts/step_summary.py $(ls gpurun_out/r04/$T/prof/*kernel_stats.csv | head -1) --steps 4 > gpurun_out/r04/$T/step_summary.txt 2>&1; head -24 gpurun_out/r04/$T/step_summary.txt

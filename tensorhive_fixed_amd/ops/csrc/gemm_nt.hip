@@ -310,6 +310,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.f);
+  // Materialise every zero accumulator in the AGPR file here, then pad: hipcc otherwise zeroes an
+  // accumulator lazily (v_accvgpr_mov) right before the first MFMA statement that reads it, and it
+  // inserts no wait states in front of an asm MFMA, so the MFMA read a stale SrcC (variant 8 returned
+  // inf before this).  The empty "+a" statements pin the values; asm volatile keeps them in order.
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4" ::);
 
   const int nt = K / BK;
   bf16x8 a0[8], b0[8], a1[8], b1[8];

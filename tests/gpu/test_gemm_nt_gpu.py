@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 D, F, HQKV, V = 4096, 14336, 6144, 128256
 
 
-def _run(M, N, K, beta, stride_pad=0, seed=0):
+def _run(M, N, K, beta, stride_pad=0, seed=0, variant=None):
     from tensorhive_fixed_amd.ops import _lib
     from tensorhive_fixed_amd.ops.gemm_nt import gemm_nt_, usable
 
@@ -20,7 +20,7 @@ def _run(M, N, K, beta, stride_pad=0, seed=0):
     c = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g)
     assert usable(a, b, c)  # the HIP kernel runs, not the fallback
     c0 = c.float().clone()
-    gemm_nt_(a, b, c, accumulate=bool(beta))
+    gemm_nt_(a, b, c, accumulate=bool(beta), variant=variant)
     torch.cuda.synchronize()
     ref = a.float() @ b.float().t() + (c0 if beta else 0)
     return ((c.float() - ref).norm() / ref.norm()).item()
@@ -39,6 +39,14 @@ def test_gemm_nt_matches_fp32(M, N, K, beta):
 def test_gemm_nt_llama_shapes(name, N, K):
     M = 512 if N * K > 200_000_000 else 1024
     assert _run(M, N, K, 0) < 5e-3, name
+
+
+@pytest.mark.parametrize("variant", [0, 1, 8, 16, 17, 20])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 512, 128), (256, 512, 4096)])
+def test_gemm_nt_schedule_variants_match_fp32(M, N, K, variant):
+    """Every compiled schedule variant (A/B aids) is exact too: a variant that read a stale
+    accumulator returned inf here before the accumulators were pinned ahead of the loop."""
+    assert _run(M, N, K, 0, variant=variant) < 5e-3
 
 
 def test_gemm_nt_output_orientation():
