@@ -96,7 +96,8 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 
 # launch flags of the backward (th_flash_attn_bwd), A/B aids: bit0 q-major dQ order; bit1 / bit2
 # fused dK/dV order / priority; bit3 the fused register-staged dK/dV kernel instead of the paired
-# half-width one; bit5 register-staged K/V tiles in dQ and the fused dK/dV kernel (the path
+# half-width one; bit4 the one-wave-per-SIMD fused dK|dV kernel with AGPR-pinned accumulators (kf,
+# S % 64 == 0; other lengths keep kh); bit5 register-staged K/V tiles in dQ and the fused dK/dV kernel (the path
 # sequences whose LDS-DMA offsets overflow 32 bits take by themselves).  The 8-wave paired kernels
 # of rounds 2-3 (old bits 6-8) are retired: profiles/r03_flash/retired_kc_kernels.patch
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", "0"))
@@ -112,7 +113,7 @@ def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.T
               rope: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
     """HIP flash attention backward -> dqkv in the packed layout.  ``rope`` = the (cos, sin) tables of
     ``ops/rope.py``: dq and dk come out with the rotary backward already applied (default dK|dV
-    kernel only, ``flags`` 0)."""
+    kernels: ``flags`` without bits 3 and 5)."""
     row = qkv.shape[1]
     if not do.is_contiguous():
         do = do.contiguous()
@@ -169,7 +170,7 @@ class _QKVAttention(torch.autograd.Function):
             # (S * row * 2 B < 2^31, flash_attn.hip flash_bwd_impl), longer rows take the
             # register-staged kernels + a separate rotary pass
             row = qkv.shape[1]
-            if _ROPE_FUSED and _BWD_FLAGS == 0 and Dh == 128 and S * row * 2 < (1 << 31):
+            if _ROPE_FUSED and not (_BWD_FLAGS & (8 | 32)) and Dh == 128 and S * row * 2 < (1 << 31):
                 tabs = rope_tables(S, Dh, theta, do.device)
                 return (flash_bwd(do, qkv, o, lse, B, S, Hq, Hkv, Dh, flags=_BWD_FLAGS, rope=tabs),
                         None, None, None, None, None, None, None)

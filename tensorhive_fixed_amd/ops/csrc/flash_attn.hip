@@ -201,7 +201,12 @@ __device__ __forceinline__ void q_block_map(int L, int nqb, int B, int Hq, int H
 // fills image byte o = 4096w + 1024u + 16l, so it loads the (row, chunk) that img_off maps to o.
 // No staging VGPRs, no ds_write, one barrier per tile (double-buffered images).
 __device__ __forceinline__ void glds16(const void* sbase, unsigned voff, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
+}
+// 4 B per lane (a 64-float row: lse / delta of a 64-query tile)
+__device__ __forceinline__ void glds4(const void* sbase, unsigned voff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2"
                :: "s"(lds), "v"(voff), "s"(sbase) : "memory", "m0");
 }
 // (row | chunk << 8) of image byte o (inverse of img_off)
@@ -1111,6 +1116,264 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_kh_kernel(
                   scale_log2, causal, rcos, rsin);
 }
 
+// ------------------------------ fused dK | dV kernel, one wave per SIMD, both roles per wave (kf)
+// kh splits each 32-key slice between a dK and a dV wave because one wave cannot hold both
+// accumulator sets beside its operands in 256 registers.  Here the dK^T and dV^T accumulators
+// (8 x f32x16 = 128 registers) sit in the AGPR half of the 512-entry file, pinned there by
+// inline-asm MFMAs ("+a" operands, as in ops/csrc/gemm_nt.hip), so ONE wave computes S, P, dP, dS,
+// dV^T and dK^T of its 32 keys:
+//   * no P exchange through LDS and one barrier per tile (kh: two);
+//   * 4 waves cover 128 keys per staged Q|dO tile (kh: 64), so half the LDS-DMA bytes per MFMA;
+//   * a 3-slot Q|dO ring, DMA two tiles ahead, the barrier in the middle of a tile so the next
+//     tile's first operands are read before this tile's MFMAs run out.
+// Per 64-query tile a wave issues 64 MFMAs (32x32x16) in one fixed order -- S|dP chains of query
+// half 0 (i = 0-15) and half 1 (16-31), then dV^T|dK^T of half 0 (32-47) and half 1 (48-63) -- with
+// each MFMA's LDS operand read three MFMAs ahead and the softmax-gradient VALU of one half spread
+// one element per MFMA gap over the next 16 MFMAs (half 0 in 16-31, half 1 in 32-47; the next
+// tile's -lse / -delta accumulator init in 48-63).  Every MFMA is inline asm: the S|dP accumulators
+// stay in VGPRs ("+v", no v_accvgpr_read before the exponentials), the dV|dK ones in AGPRs.
+// ring slot: Q | dO | lse | delta as in KC_TILE + 512 B where waves 2-3 drop their copy of the lse /
+// delta load (every wave issues the same DMA sequence: no branch in the loop body)
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N), fully expanded (a 64-step
+// #pragma unroll body exceeds clang's unroll size threshold and stays a runtime loop)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+constexpr int KF_BK = 128, KF_STAGES = 3, KF_TILE = KC_TILE + 512, KF_LDS = KF_STAGES * KF_TILE;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// s_nop 1: A/B/C may be fresh VALU results (packed P / dS, the -lse init); hipcc pads nothing in
+// front of an asm statement (cdna_hip_programming.md 5.7 item 2).  D -> next MFMA as C: 0 states.
+__device__ __forceinline__ void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+
+// VAR bit0: the next tile's lse / delta read from LDS right after the mid-tile barrier and converted
+// four gaps later (default: read and converted in one gap, whose VALU then waits on the reads);
+// bit1: the causal mask applied to the S' chain's initial C (-inf where key > query) in the
+// nearly idle gaps 48-63 instead of to P in the softmax gaps 16-47
+// (exp2(-inf + finite) = 0, and dS = 0 * dP' stays 0)
+template <int VAR>
+__global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal, const float* __restrict__ rcos,
+    const float* __restrict__ rsin) {
+  __shared__ __attribute__((aligned(1024))) char smem[KF_LDS];
+  const int nkb = (S + KF_BK - 1) / KF_BK;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = L / nkb, kb_i = L % nkb;  // (batch, kv head)-major, heaviest key block first
+  const int b = grp / Hkv, hk = grp % Hkv;
+  const int kblk0 = (causal ? kb_i : nkb - 1 - kb_i) * KF_BK;
+  const int G = Hq / Hkv;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k0 = kblk0 + 32 * w;
+  const int key = k0 + c32;
+  // K (prescaled by softmax_scale * log2 e: S' = Q K'^T - lse2 is a log2-domain score) and V
+  // fragments of this wave's 32 keys, for the whole kernel
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    ushort8 u = key < S ? *reinterpret_cast<const ushort8*>(Kb + (long)key * ld + 16 * s + 8 * h) : ushort8(0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
+    kf[s] = as_bf(u);
+    vf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(Vb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
+  }
+  f32x16 ak[4], av[4];  // dK^T, dV^T: 128 head dims (4 x 32 accumulator rows) x 32 keys (lanes)
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    ak[d] = f32x16(0.f);
+    av[d] = f32x16(0.f);
+  }
+  // the zeros materialised in the AGPRs here, with a pad before the first asm MFMA reads them
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    asm volatile("" : "+a"(ak[d]));
+    asm volatile("" : "+a"(av[d]));
+  }
+  asm volatile("s_nop 4" ::);
+
+  const int nqt = S / C_BQ;  // host: S % 64 == 0
+  const int qt0 = causal ? kblk0 / C_BQ : 0;
+  const int per_head = nqt - qt0;
+  const int total = G * per_head;
+  // Tile DMA into a ring slot: waves 0-1 stage Q, waves 2-3 dO (8 x 1 KB per wave); wave 0 also
+  // the tile's 64 lse, wave 1 its 64 delta (raw; waves 2-3 the same into the spare), issued FIRST, so one vmcnt(9) per wave means "my
+  // pieces of the older tile landed" on every wave.  Tile index clamped (branch-free loop body):
+  // a DMA past the last tile re-loads it into a slot nobody reads again.
+  unsigned rc[8];
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
+  auto dma_tile = [&](int j, int slot) {
+    j = min(j, total - 1);
+    const int h_i = j / per_head, t_i = j - h_i * per_head;
+    const int hq = hk * G + h_i;
+    const int qq0 = (qt0 + t_i) * C_BQ;
+    const bool isq = w < 2;
+    const ushort* base = isq ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
+    const long ldx = isq ? ld : ldo;
+    const unsigned slot0 = __builtin_amdgcn_readfirstlane(lds0 + slot * KF_TILE);
+    const float* lb = ((w & 1) ? Dl : LSE) + ((long)b * Hq + hq) * S + qq0;
+    glds4(lb, (unsigned)lane * 4u, slot0 + 2 * C_BQ * 256 + w * (C_BQ * 4));
+    const unsigned img = slot0 + (isq ? 0 : C_BQ * 256) + (w & 1) * 8192;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = qq0 + (int)(rc[u] & 255);
+      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
+    }
+  };
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // K/V fragment loads retired (a wait the compiler sees)
+  {
+    const int wq = w & 1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) rc[u] = img_rc(wq * 8192 + u * 1024 + lane * 16);
+  }
+  dma_tile(0, 0);
+  dma_tile(1, 1);
+  asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");  // tile 0 landed everywhere
+
+  // operand of MFMA i (0-63) of the tile staged at `slot`
+  auto opnd = [&](int i, const char* qs) -> bf16x8 {
+    const char* gs = qs + C_BQ * 256;
+    if (i < 32) {
+      const int kb = i >> 4, j = (i & 15) >> 1;
+      return lds_row((i & 1) ? gs : qs, 32 * kb + c32, 2 * j + h);
+    }
+    const int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
+    return lds_tr(sub < 2 ? gs : qs, 32 * kb + 16 * (sub & 1), 32 * d, lane);
+  };
+  // -lse2 / -delta of query half kb (accumulator row order) as the S' / dP' chains' initial C
+  f32x16 cs[2], cp[2];
+  // (VAR bit1) -inf where key > query: mt = key - (first query of the tile) - 4h, or < -64
+  auto masked = [&](float x, int mt, int kb, int g, int e) {
+    return (VAR & 2) && mt - 32 * kb > e + 8 * g ? -INFINITY : x;
+  };
+  auto init_c = [&](int kb, const char* qs, int mt) {
+    const float* rl = reinterpret_cast<const float*>(qs + 2 * C_BQ * 256) + 32 * kb + 4 * h;
+    const float* rd = rl + C_BQ;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4v l = *reinterpret_cast<const float4v*>(rl + 8 * g);
+      const float4v dl = *reinterpret_cast<const float4v*>(rd + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const f32x2 lv = f32x2{l[e], l[e + 1]} * f32x2{-LOG2E, -LOG2E};
+        const f32x2 dv = f32x2{dl[e], dl[e + 1]} * f32x2{-1.f, -1.f};
+        cs[kb][4 * g + e] = masked(lv[0], mt, kb, g, e);
+        cs[kb][4 * g + e + 1] = masked(lv[1], mt, kb, g, e + 1);
+        cp[kb][4 * g + e] = dv[0];
+        cp[kb][4 * g + e + 1] = dv[1];
+      }
+    }
+  };
+  float4v lraw[2][4], draw[2][4];
+  auto load_c = [&](int kb, const char* qs) {
+    const float* rl = reinterpret_cast<const float*>(qs + 2 * C_BQ * 256) + 32 * kb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      lraw[kb][g] = *reinterpret_cast<const float4v*>(rl + 8 * g);
+      draw[kb][g] = *reinterpret_cast<const float4v*>(rl + C_BQ + 8 * g);
+    }
+  };
+  auto conv_c = [&](int kb, int g, int mt) {
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      const f32x2 lv = f32x2{lraw[kb][g][e], lraw[kb][g][e + 1]} * f32x2{-LOG2E, -LOG2E};
+      const f32x2 dv = f32x2{draw[kb][g][e], draw[kb][g][e + 1]} * f32x2{-1.f, -1.f};
+      cs[kb][4 * g + e] = masked(lv[0], mt, kb, g, e);
+      cs[kb][4 * g + e + 1] = masked(lv[1], mt, kb, g, e + 1);
+      cp[kb][4 * g + e] = dv[0];
+      cp[kb][4 * g + e + 1] = dv[1];
+    }
+  };
+  // P = exp2(S') (0 where key > query), dS = P dP', packed to the bf16 B operands of the dV / dK
+  // chains: element r of half kb
+  bf16x8 pp[2][2], sp[2][2];
+  int mthr = 0;
+  auto softmax_elem = [&](int kb, int r) {
+    const float pv = !(VAR & 2) && mthr - 32 * kb > (r & 3) + 8 * (r >> 2) ? 0.f : fast_exp2(cs[kb][r]);
+    const float dsv = pv * cp[kb][r];
+    pp[kb][r >> 3][r & 7] = (__bf16)pv;
+    sp[kb][r >> 3][r & 7] = (__bf16)dsv;
+  };
+
+  // key - first query of tile t - 4h (causal), or a value no row constant exceeds
+  auto mt_of = [&](int t) { return causal ? key - (qt0 + t % per_head) * C_BQ - 4 * h : -128; };
+  const char* cur = smem;
+  init_c(0, cur, mt_of(0));
+  init_c(1, cur, mt_of(0));
+  bf16x8 opr[4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) opr[i] = opnd(i, cur);
+  for (int it = 0; it < total; ++it) {
+    const char* nxt = smem + ((it + 1) % KF_STAGES) * KF_TILE;
+    mthr = mt_of(it);  // causal: mask where key > query
+    const int mnext = mt_of(it + 1);
+    static_for<0, 64>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i == 48) {
+        // this wave's DMA of tile it+1 landed, the barrier makes every wave's visible and puts
+        // everyone past tile it-1, whose slot (it+2) % 3 takes tile it+2
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        dma_tile(it + 2, (it + 2) % KF_STAGES);
+      }
+      constexpr int ni = i + 3;
+      const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 a = opr[i & 3];
+      if constexpr (i < 32) {
+        constexpr int kb = i >> 4, j = (i & 15) >> 1;
+        if constexpr (i & 1) mfma_v(cp[kb], a, vf[j]);
+        else mfma_v(cs[kb], a, kf[j]);
+      } else {
+        constexpr int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
+        if constexpr (sub < 2) mfma_a(av[d], a, pp[kb][sub]);
+        else mfma_a(ak[d], a, sp[kb][sub & 1]);
+      }
+      // VALU of the gap
+      if constexpr (i == 16 || i == 32) {
+        // the S' / dP' chain of the half just finished: its last MFMA's D -> VALU read (8-pass XDL)
+        const int kb = (i >> 4) - 1;
+        asm volatile("s_nop 7\n\ts_nop 3" : "+v"(cs[kb]), "+v"(cp[kb]));
+      }
+      if constexpr (i >= 16 && i < 48) softmax_elem((i >> 4) - 1, i & 15);
+      if constexpr (VAR & 1) {
+        if constexpr (i == 48) load_c(0, nxt);
+        if constexpr (i == 50) load_c(1, nxt);
+        if constexpr (i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext);
+      } else {
+        if constexpr (i == 48) init_c(0, nxt, mnext);
+        if constexpr (i == 52) init_c(1, nxt, mnext);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      opr[(i + 3) & 3] = nx;
+    });
+    cur = nxt;
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    asm volatile("" : "+a"(ak[d]));
+    asm volatile("" : "+a"(av[d]));
+  }
+  if (key < S) {
+    if (rcos != nullptr) rope_bwd_rows(ak, rcos, rsin, key, h);  // dK rows: rotary backward
+    store_row_t21(dK + b * bs + (long)key * ld + (long)hk * HD, ak, scale, h);
+    store_row_t21(dV + b * bs + (long)key * ld + (long)hk * HD, av, 1.f, h);
+  }
+}
+
 constexpr int B_LDS = 2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4;
 }  // namespace
 
@@ -1161,6 +1424,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
   if (rcos != nullptr && ((flags & (8 | 32)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
     return -3;
+  if ((flags & 16) && S % C_BQ != 0) flags &= ~16;  // kf assumes whole 64-query tiles: kh instead
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
   // bit5: register-staged K/V tiles instead of LDS-DMA (also used when 32-bit offsets overflow)
@@ -1179,6 +1443,22 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
 #undef TH_DQ_LAUNCH
   // default: the half-width paired dK|dV kernel (two workgroups per CU, profiles/r03_flash); flags
   // bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused register-staged dK/dV kernel below
+  if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
+    const long nkf = (long)((S + KF_BK - 1) / KF_BK) * Hkv * B;
+#define TH_KF_LAUNCH(V_)                                                                                      \
+  fa_bwd_kf_kernel<V_><<<(unsigned)nkf, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,        \
+                                                     (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,   \
+                                                     B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, \
+                                                     rcos, rsin)
+    switch ((flags >> 6) & 3) {  // bits 6-7: kf variant
+      case 1: TH_KF_LAUNCH(1); break;
+      case 2: TH_KF_LAUNCH(2); break;
+      case 3: TH_KF_LAUNCH(3); break;
+      default: TH_KF_LAUNCH(0);
+    }
+#undef TH_KF_LAUNCH
+    TH_CHECK_LAUNCH();
+  }
   if (!(flags & 8) && dq_dma) {
     const long nkh = (long)((S + KH_BK - 1) / KH_BK) * Hkv * B;
     fa_bwd_kh_kernel<<<(unsigned)nkh, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
