@@ -1144,35 +1144,41 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 constexpr int KF_BK = 128, KF_STAGES = 3, KF_TILE = KC_TILE + 512, KF_LDS = KF_STAGES * KF_TILE;
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // s_nop 1: A/B/C may be fresh VALU results (packed P / dS, the -lse init); hipcc pads nothing in
 // front of an asm statement (cdna_hip_programming.md 5.7 item 2).  D -> next MFMA as C: 0 states.
+template <bool PAD>
 __device__ __forceinline__ void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  if constexpr (PAD)
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
+template <bool PAD>
 __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  if constexpr (PAD)
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  else
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
 
 // VAR bit0: the next tile's lse / delta read from LDS right after the mid-tile barrier and converted
 // four gaps later (default: read and converted in one gap, whose VALU then waits on the reads);
 // bit1: the causal mask applied to the S' chain's initial C (-inf where key > query) in the
 // nearly idle gaps 48-63 instead of to P in the softmax gaps 16-47
-// (exp2(-inf + finite) = 0, and dS = 0 * dP' stays 0)
+// (exp2(-inf + finite) = 0, and dS = 0 * dP' stays 0); bit2: the 9 DMA pieces of tile it+2 issued
+// one per MFMA gap (48-56) instead of all in gap 48 (a piece costs the issuing wave ~60-185 cycles,
+// MI355X_MICROARCH 'LDS-DMA piece issue cost'); bit3: the 2-state VALU -> MFMA pad only in front of
+// the MFMAs whose B / C operand a recent gap wrote (0, 16, 32, 33, 48, 49), not all 64; bit4:
+// operands read 6 MFMAs ahead instead of 3
+// one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
 template <int VAR>
-__global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
+__device__ __forceinline__ void kf_block(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
     ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
     long bs, long ldo, long bso, float scale, float scale_log2, int causal, const float* __restrict__ rcos,
-    const float* __restrict__ rsin) {
-  __shared__ __attribute__((aligned(1024))) char smem[KF_LDS];
-  const int nkb = (S + KF_BK - 1) / KF_BK;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int grp = L / nkb, kb_i = L % nkb;  // (batch, kv head)-major, heaviest key block first
-  const int b = grp / Hkv, hk = grp % Hkv;
-  const int kblk0 = (causal ? kb_i : nkb - 1 - kb_i) * KF_BK;
+    const float* __restrict__ rsin, char* smem, int b, int hk, int kblk0) {
   const int G = Hq / Hkv;
   const ushort* Kb = K + b * bs + (long)hk * HD;
   const ushort* Vb = V + b * bs + (long)hk * HD;
@@ -1215,23 +1221,38 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
   // a DMA past the last tile re-loads it into a slot nobody reads again.
   unsigned rc[8];
   const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
-  auto dma_tile = [&](int j, int slot) {
+  // DMA of one tile in pieces: dma_prep(j, slot) picks the source rows, dma_piece(u) issues piece u
+  // (u = 0: the lse / delta row, 1-8: the 1 KB Q or dO pieces)
+  const ushort* d_base = Q;
+  const float* d_lb = LSE;
+  unsigned d_slot0 = 0, d_img = 0;
+  int d_qq0 = 0;
+  long d_ldx = ld;
+  auto dma_prep = [&](int j, int slot) {
     j = min(j, total - 1);
     const int h_i = j / per_head, t_i = j - h_i * per_head;
     const int hq = hk * G + h_i;
-    const int qq0 = (qt0 + t_i) * C_BQ;
+    d_qq0 = (qt0 + t_i) * C_BQ;
     const bool isq = w < 2;
-    const ushort* base = isq ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
-    const long ldx = isq ? ld : ldo;
-    const unsigned slot0 = __builtin_amdgcn_readfirstlane(lds0 + slot * KF_TILE);
-    const float* lb = ((w & 1) ? Dl : LSE) + ((long)b * Hq + hq) * S + qq0;
-    glds4(lb, (unsigned)lane * 4u, slot0 + 2 * C_BQ * 256 + w * (C_BQ * 4));
-    const unsigned img = slot0 + (isq ? 0 : C_BQ * 256) + (w & 1) * 8192;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int row = qq0 + (int)(rc[u] & 255);
-      glds16(base, (unsigned)(row * ldx + (rc[u] >> 8) * 8) * 2u, img + u * 1024);
+    d_base = isq ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
+    d_ldx = isq ? ld : ldo;
+    d_slot0 = __builtin_amdgcn_readfirstlane(lds0 + slot * KF_TILE);
+    d_lb = ((w & 1) ? Dl : LSE) + ((long)b * Hq + hq) * S + d_qq0;
+    d_img = d_slot0 + (isq ? 0 : C_BQ * 256) + (w & 1) * 8192;
+  };
+  auto dma_piece = [&](int u) {
+    if (u == 0) {
+      glds4(d_lb, (unsigned)lane * 4u, d_slot0 + 2 * C_BQ * 256 + w * (C_BQ * 4));
+    } else {
+      const unsigned r = rc[u - 1];
+      const int row = d_qq0 + (int)(r & 255);
+      glds16(d_base, (unsigned)(row * d_ldx + (r >> 8) * 8) * 2u, d_img + (u - 1) * 1024);
     }
+  };
+  auto dma_tile = [&](int j, int slot) {
+    dma_prep(j, slot);
+#pragma unroll
+    for (int u = 0; u < 9; ++u) dma_piece(u);
   };
   __builtin_amdgcn_s_waitcnt(0x0F70);  // K/V fragment loads retired (a wait the compiler sees)
   {
@@ -1267,13 +1288,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
       const float4v l = *reinterpret_cast<const float4v*>(rl + 8 * g);
       const float4v dl = *reinterpret_cast<const float4v*>(rd + 8 * g);
 #pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const f32x2 lv = f32x2{l[e], l[e + 1]} * f32x2{-LOG2E, -LOG2E};
-        const f32x2 dv = f32x2{dl[e], dl[e + 1]} * f32x2{-1.f, -1.f};
-        cs[kb][4 * g + e] = masked(lv[0], mt, kb, g, e);
-        cs[kb][4 * g + e + 1] = masked(lv[1], mt, kb, g, e + 1);
-        cp[kb][4 * g + e] = dv[0];
-        cp[kb][4 * g + e + 1] = dv[1];
+      for (int e = 0; e < 4; ++e) {  // scalar: packed f32 VALU is an anti-lever beside MFMAs
+        cs[kb][4 * g + e] = masked(l[e] * -LOG2E, mt, kb, g, e);
+        cp[kb][4 * g + e] = -dl[e];
       }
     }
   };
@@ -1288,13 +1305,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
   };
   auto conv_c = [&](int kb, int g, int mt) {
 #pragma unroll
-    for (int e = 0; e < 4; e += 2) {
-      const f32x2 lv = f32x2{lraw[kb][g][e], lraw[kb][g][e + 1]} * f32x2{-LOG2E, -LOG2E};
-      const f32x2 dv = f32x2{draw[kb][g][e], draw[kb][g][e + 1]} * f32x2{-1.f, -1.f};
-      cs[kb][4 * g + e] = masked(lv[0], mt, kb, g, e);
-      cs[kb][4 * g + e + 1] = masked(lv[1], mt, kb, g, e + 1);
-      cp[kb][4 * g + e] = dv[0];
-      cp[kb][4 * g + e + 1] = dv[1];
+    for (int e = 0; e < 4; ++e) {
+      cs[kb][4 * g + e] = masked(lraw[kb][g][e] * -LOG2E, mt, kb, g, e);
+      cp[kb][4 * g + e] = -draw[kb][g][e];
     }
   };
   // P = exp2(S') (0 where key > query), dS = P dP', packed to the bf16 B operands of the dV / dK
@@ -1313,9 +1326,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
   const char* cur = smem;
   init_c(0, cur, mt_of(0));
   init_c(1, cur, mt_of(0));
-  bf16x8 opr[4];
+  constexpr int PD = (VAR & 16) ? 6 : 3, NR = (VAR & 16) ? 8 : 4;  // read distance, operand ring
+  bf16x8 opr[NR];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) opr[i] = opnd(i, cur);
+  for (int i = 0; i < PD; ++i) opr[i] = opnd(i, cur);
   for (int it = 0; it < total; ++it) {
     const char* nxt = smem + ((it + 1) % KF_STAGES) * KF_TILE;
     mthr = mt_of(it);  // causal: mask where key > query
@@ -1326,20 +1340,25 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
         // this wave's DMA of tile it+1 landed, the barrier makes every wave's visible and puts
         // everyone past tile it-1, whose slot (it+2) % 3 takes tile it+2
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        dma_tile(it + 2, (it + 2) % KF_STAGES);
+        if constexpr (VAR & 4)
+          dma_prep(it + 2, (it + 2) % KF_STAGES);
+        else
+          dma_tile(it + 2, (it + 2) % KF_STAGES);
       }
-      constexpr int ni = i + 3;
+      if constexpr ((VAR & 4) && i >= 48 && i < 57) dma_piece(i - 48);
+      constexpr int ni = i + PD;
       const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 a = opr[i & 3];
+      const bf16x8 a = opr[i % NR];
+      constexpr bool pad = !(VAR & 8) || i == 0 || i == 16 || i == 32 || i == 33 || i == 48 || i == 49;
       if constexpr (i < 32) {
         constexpr int kb = i >> 4, j = (i & 15) >> 1;
-        if constexpr (i & 1) mfma_v(cp[kb], a, vf[j]);
-        else mfma_v(cs[kb], a, kf[j]);
+        if constexpr (i & 1) mfma_v<pad>(cp[kb], a, vf[j]);
+        else mfma_v<pad>(cs[kb], a, kf[j]);
       } else {
         constexpr int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
-        if constexpr (sub < 2) mfma_a(av[d], a, pp[kb][sub]);
-        else mfma_a(ak[d], a, sp[kb][sub & 1]);
+        if constexpr (sub < 2) mfma_a<pad>(av[d], a, pp[kb][sub]);
+        else mfma_a<pad>(ak[d], a, sp[kb][sub & 1]);
       }
       // VALU of the gap
       if constexpr (i == 16 || i == 32) {
@@ -1357,7 +1376,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
         if constexpr (i == 52) init_c(1, nxt, mnext);
       }
       __builtin_amdgcn_sched_barrier(0);
-      opr[(i + 3) & 3] = nx;
+      opr[(i + PD) % NR] = nx;
     });
     cur = nxt;
   }
@@ -1371,6 +1390,40 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
     if (rcos != nullptr) rope_bwd_rows(ak, rcos, rsin, key, h);  // dK rows: rotary backward
     store_row_t21(dK + b * bs + (long)key * ld + (long)hk * HD, ak, scale, h);
     store_row_t21(dV + b * bs + (long)key * ld + (long)hk * HD, av, 1.f, h);
+  }
+}
+
+
+// VAR bit5: each workgroup takes the key-block pair (i, nkb-1-i) one after the other -- under a
+// causal mask every pair carries the same number of tiles, so the grid is one uniform size
+// instead of a 32:1 spread whose heavy blocks may start last on a CU
+template <int VAR>
+__global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    const ushort* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Dl,
+    ushort* __restrict__ dK, ushort* __restrict__ dV, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale, float scale_log2, int causal, const float* __restrict__ rcos,
+    const float* __restrict__ rsin) {
+  __shared__ __attribute__((aligned(1024))) char smem[KF_LDS];
+  const int nkb = (S + KF_BK - 1) / KF_BK;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  if constexpr (VAR & 32) {
+    const int np = (nkb + 1) / 2;
+    const int grp = L / np, kb_i = L % np;
+    const int b = grp / Hkv, hk = grp % Hkv;
+    kf_block<VAR>(Q, K, V, dO, LSE, Dl, dK, dV, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale_log2, causal, rcos,
+                  rsin, smem, b, hk, kb_i * KF_BK);
+    const int kb2 = nkb - 1 - kb_i;
+    if (kb2 != kb_i) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done with the ring
+      kf_block<VAR>(Q, K, V, dO, LSE, Dl, dK, dV, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale_log2, causal,
+                    rcos, rsin, smem, b, hk, kb2 * KF_BK);
+    }
+  } else {
+    const int grp = L / nkb, kb_i = L % nkb;  // (batch, kv head)-major, heaviest key block first
+    const int b = grp / Hkv, hk = grp % Hkv;
+    kf_block<VAR>(Q, K, V, dO, LSE, Dl, dK, dV, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale_log2, causal, rcos,
+                  rsin, smem, b, hk, (causal ? kb_i : nkb - 1 - kb_i) * KF_BK);
   }
 }
 
@@ -1444,16 +1497,24 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // default: the half-width paired dK|dV kernel (two workgroups per CU, profiles/r03_flash); flags
   // bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
-    const long nkf = (long)((S + KF_BK - 1) / KF_BK) * Hkv * B;
+    const int kvar = (flags >> 6) & 63;  // bits 6-11: kf variant (VAR)
+    const int nkb_f = (S + KF_BK - 1) / KF_BK;
+    const long nkf = (long)((kvar & 32) ? (nkb_f + 1) / 2 : nkb_f) * Hkv * B;
 #define TH_KF_LAUNCH(V_)                                                                                      \
   fa_bwd_kf_kernel<V_><<<(unsigned)nkf, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,        \
                                                      (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,   \
                                                      B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, \
                                                      rcos, rsin)
-    switch ((flags >> 6) & 3) {  // bits 6-7: kf variant
-      case 1: TH_KF_LAUNCH(1); break;
-      case 2: TH_KF_LAUNCH(2); break;
+    switch (kvar) {
       case 3: TH_KF_LAUNCH(3); break;
+      case 35: TH_KF_LAUNCH(35); break;
+      case 47: TH_KF_LAUNCH(47); break;
+      case 63: TH_KF_LAUNCH(63); break;
+      case 7: TH_KF_LAUNCH(7); break;
+      case 11: TH_KF_LAUNCH(11); break;
+      case 15: TH_KF_LAUNCH(15); break;
+      case 19: TH_KF_LAUNCH(19); break;
+      case 31: TH_KF_LAUNCH(31); break;
       default: TH_KF_LAUNCH(0);
     }
 #undef TH_KF_LAUNCH
