@@ -1170,7 +1170,8 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
 // one per MFMA gap (48-56) instead of all in gap 48 (a piece costs the issuing wave ~60-185 cycles,
 // MI355X_MICROARCH 'LDS-DMA piece issue cost'); bit3: the 2-state VALU -> MFMA pad only in front of
 // the MFMAs whose B / C operand a recent gap wrote (0, 16, 32, 33, 48, 49), not all 64; bit4:
-// operands read 6 MFMAs ahead instead of 3
+// operands read 6 MFMAs ahead instead of 3; bit6: the barrier and the DMA pieces at the start of
+// the tile, in the gaps of half 0's S|dP chains, which carry no softmax VALU (default: step 48)
 // one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
 template <int VAR>
 __device__ __forceinline__ void kf_block(
@@ -1327,6 +1328,7 @@ __device__ __forceinline__ void kf_block(
   init_c(0, cur, mt_of(0));
   init_c(1, cur, mt_of(0));
   constexpr int PD = (VAR & 16) ? 6 : 3, NR = (VAR & 16) ? 8 : 4;  // read distance, operand ring
+  constexpr int BAR = (VAR & 64) ? 0 : 48;  // MFMA step of the per-tile barrier + tile it+2's DMA
   bf16x8 opr[NR];
 #pragma unroll
   for (int i = 0; i < PD; ++i) opr[i] = opnd(i, cur);
@@ -1336,7 +1338,7 @@ __device__ __forceinline__ void kf_block(
     const int mnext = mt_of(it + 1);
     static_for<0, 64>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      if constexpr (i == 48) {
+      if constexpr (i == BAR) {
         // this wave's DMA of tile it+1 landed, the barrier makes every wave's visible and puts
         // everyone past tile it-1, whose slot (it+2) % 3 takes tile it+2
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1345,7 +1347,7 @@ __device__ __forceinline__ void kf_block(
         else
           dma_tile(it + 2, (it + 2) % KF_STAGES);
       }
-      if constexpr ((VAR & 4) && i >= 48 && i < 57) dma_piece(i - 48);
+      if constexpr ((VAR & 4) && i >= BAR && i < BAR + 9) dma_piece(i - BAR);
       constexpr int ni = i + PD;
       const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
       __builtin_amdgcn_sched_barrier(0);
@@ -1497,7 +1499,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // default: the half-width paired dK|dV kernel (two workgroups per CU, profiles/r03_flash); flags
   // bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
-    const int kvar = (flags >> 6) & 63;  // bits 6-11: kf variant (VAR)
+    const int kvar = (flags >> 6) & 127;  // bits 6-12: kf variant (VAR)
     const int nkb_f = (S + KF_BK - 1) / KF_BK;
     const long nkf = (long)((kvar & 32) ? (nkb_f + 1) / 2 : nkb_f) * Hkv * B;
 #define TH_KF_LAUNCH(V_)                                                                                      \
@@ -1510,6 +1512,9 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
       case 35: TH_KF_LAUNCH(35); break;
       case 47: TH_KF_LAUNCH(47); break;
       case 63: TH_KF_LAUNCH(63); break;
+      case 108: TH_KF_LAUNCH(108); break;
+      case 111: TH_KF_LAUNCH(111); break;
+      case 110: TH_KF_LAUNCH(110); break;
       case 7: TH_KF_LAUNCH(7); break;
       case 11: TH_KF_LAUNCH(11); break;
       case 15: TH_KF_LAUNCH(15); break;

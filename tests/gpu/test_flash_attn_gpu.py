@@ -13,9 +13,9 @@ def _ref(qkv, B, S, Hq, Hkv, D, causal=True):
     return attention_reference(q, k, v, causal).reshape(B * S, Hq * D)
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 208, 976, 2000, 3024, 4048, 32],
-                         ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v3", "kf_v15", "kf_v31", "kf_v47",
-                              "kf_v63", "regstage"])
+@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 976, 3024, 6928, 7120, 32],
+                         ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v15", "kf_v47", "kf_v108", "kf_v111",
+                              "regstage"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 128, 4, 1), (2, 200, 8, 2), (1, 1024, 32, 8), (1, 64, 2, 2)])
 def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -64,9 +64,9 @@ def test_qkv_attention_with_rope_matches_sdpa_path():
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 208, 976, 2000, 3024, 4048, 32],
-                         ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v3", "kf_v15", "kf_v31", "kf_v47",
-                              "kf_v63", "regstage"])
+@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 976, 3024, 6928, 7120, 32],
+                         ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v15", "kf_v47", "kf_v108", "kf_v111",
+                              "regstage"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 200, 8, 2), (1, 384, 4, 4)])
 def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
