@@ -100,7 +100,11 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 # S % 64 == 0; other lengths keep kh); bit5 register-staged K/V tiles in dQ and the fused dK/dV kernel (the path
 # sequences whose LDS-DMA offsets overflow 32 bits take by themselves).  The 8-wave paired kernels
 # of rounds 2-3 (old bits 6-8) are retired: profiles/r03_flash/retired_kc_kernels.patch
-_BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", "0"))
+# Default: kf variant 111 (every bit-0..6 option: lse prefetch, mask in the initial C, per-gap DMA
+# pieces, selective pads, paired key blocks, barrier at the tile start): dK|dV kernel 1072 vs 1133 us
+# for kh at B4 S4096 (profiles/r04_flash/).  0 selects kh.
+KF_DEFAULT_FLAGS = 16 | (111 << 6)
+_BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", str(KF_DEFAULT_FLAGS)))
 
 
 # TH_FA_ROPE_FUSED=0: the rotary backward of dq / dk as its own in-place pass after the attention
@@ -109,12 +113,14 @@ _ROPE_FUSED = os.environ.get("TH_FA_ROPE_FUSED", "1") == "1"
 
 
 def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor, B: int,
-              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True, flags: int = 0,
+              S: int, Hq: int, Hkv: int, Dh: int, causal: bool = True, flags: int | None = None,
               rope: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
     """HIP flash attention backward -> dqkv in the packed layout.  ``rope`` = the (cos, sin) tables of
     ``ops/rope.py``: dq and dk come out with the rotary backward already applied (default dK|dV
     kernels: ``flags`` without bits 3 and 5)."""
     row = qkv.shape[1]
+    if flags is None:
+        flags = _BWD_FLAGS  # kf (flash_attn.hip falls back to kh when S % 64 != 0)
     if not do.is_contiguous():
         do = do.contiguous()
     dqkv = torch.empty_like(qkv)

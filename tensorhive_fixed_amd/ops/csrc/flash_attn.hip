@@ -1496,8 +1496,10 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     if (dq_dma) TH_DQ_LAUNCH(true, true); else TH_DQ_LAUNCH(true, false);
   }
 #undef TH_DQ_LAUNCH
-  // default: the half-width paired dK|dV kernel (two workgroups per CU, profiles/r03_flash); flags
-  // bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused register-staged dK/dV kernel below
+  // bit4 (ops/attention.py's default, with a kf variant in bits 6-12): the one-wave-per-SIMD kf
+  // kernel (profiles/r04_flash); flags 0: the half-width paired dK|dV kernel kh (two workgroups per
+  // CU, profiles/r03_flash); bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused
+  // register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
     const int kvar = (flags >> 6) & 127;  // bits 6-12: kf variant (VAR)
     const int nkb_f = (S + KF_BK - 1) / KF_BK;
@@ -1508,18 +1510,9 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
                                                      B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, \
                                                      rcos, rsin)
     switch (kvar) {
-      case 3: TH_KF_LAUNCH(3); break;
-      case 35: TH_KF_LAUNCH(35); break;
-      case 47: TH_KF_LAUNCH(47); break;
-      case 63: TH_KF_LAUNCH(63); break;
-      case 108: TH_KF_LAUNCH(108); break;
-      case 111: TH_KF_LAUNCH(111); break;
-      case 110: TH_KF_LAUNCH(110); break;
-      case 7: TH_KF_LAUNCH(7); break;
-      case 11: TH_KF_LAUNCH(11); break;
-      case 15: TH_KF_LAUNCH(15); break;
-      case 19: TH_KF_LAUNCH(19); break;
-      case 31: TH_KF_LAUNCH(31); break;
+      case 15: TH_KF_LAUNCH(15); break;   // bits 0-3
+      case 47: TH_KF_LAUNCH(47); break;   // + paired blocks
+      case 111: TH_KF_LAUNCH(111); break;  // + barrier / DMA at the tile start (the default, attention.py)
       default: TH_KF_LAUNCH(0);
     }
 #undef TH_KF_LAUNCH
