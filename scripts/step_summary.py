@@ -6,7 +6,7 @@ import csv
 from collections import defaultdict
 
 CATS = [("gemm (hipBLASLt)", ("Cijk_", "Custom_Cijk")), ("gemm TN (gfx950)", ("gemm_tn",)),
-        ("attention fwd", ("fa_fwd",)), ("attention dQ", ("fa_bwd_dq",)), ("attention dK/dV", ("fa_bwd_dkv", "fa_bwd_kc", "fa_bwd_kh")),
+        ("attention fwd", ("fa_fwd",)), ("attention dQ", ("fa_bwd_dq",)), ("attention dK/dV", ("fa_bwd_dkv", "fa_bwd_kc", "fa_bwd_kh", "fa_bwd_kf")),
         ("attention delta", ("fa_delta",)), ("transpose", ("transpose",)), ("adamw+grad-norm", ("adamw", "sumsq", "final_sum")),
         ("swiglu", ("swiglu",)), ("rmsnorm", ("rmsnorm", "slab_reduce")), ("rope", ("rope",)),
         ("cross-entropy", ("ce_fwd",)), ("embedding", ("emb_",)), ("split-K reduce", ("splitk_reduce",))]
