@@ -17,3 +17,7 @@ if [ -n "$KF_PROF" ]; then
   FA_FLAGS=${KF_FLAGS:-0,16} timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $OUT/pmc -o run -- python3 scripts/fa_bwd_ab.py > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
   python3 scripts/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt; cat $OUT/pmc_summary.txt
 fi
+if [ -n "$KF_STAMPS" ]; then
+  timeout -k 10 200 python -u scripts/kf_stamps.py > $OUT/stamps.log 2>&1 || { tail -20 $OUT/stamps.log; exit 1; }
+  cat $OUT/stamps.log
+fi

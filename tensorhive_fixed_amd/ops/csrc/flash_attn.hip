@@ -1172,6 +1172,21 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
 // the MFMAs whose B / C operand a recent gap wrote (0, 16, 32, 33, 48, 49), not all 64; bit4:
 // operands read 6 MFMAs ahead instead of 3; bit6: the barrier and the DMA pieces at the start of
 // the tile, in the gaps of half 0's S|dP chains, which carry no softmax VALU (default: step 48)
+// VAR bit7 (diagnostic builds only): s_memtime stamps per tile phase, summed over all waves into
+// g_kf_stamp = {barrier + DMA wait, MFMA 0-15, 16-31, 32-47, 48-63, wave-tiles, wave-blocks,
+// whole-block cycles}, s_memtime ticks (= shader cycles) summed over waves
+__device__ unsigned long long g_kf_stamp[8];
+// one stamp: s_memtime with its own lgkmcnt(0) in the same statement (cdna_hip_programming.md
+// 'In-kernel stamps'; read the SHARES of a stamped build, not its length)
+__device__ __forceinline__ unsigned long long kf_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define BAR_OF(V) (((V) & 64) ? 0 : 48)
+
 // one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
 template <int VAR>
 __device__ __forceinline__ void kf_block(
@@ -1324,11 +1339,17 @@ __device__ __forceinline__ void kf_block(
 
   // key - first query of tile t - 4h (causal), or a value no row constant exceeds
   auto mt_of = [&](int t) { return causal ? key - (qt0 + t % per_head) * C_BQ - 4 * h : -128; };
+  constexpr bool STAMP = (VAR & 128) != 0;
+  unsigned long long st_t0 = 0, st_prev = 0;
+  unsigned st_acc[5] = {0, 0, 0, 0, 0};
+  unsigned long long st_ts[4] = {0, 0, 0, 0};
+  static_assert(!STAMP || BAR_OF(VAR) == 0, "stamps assume the barrier at the tile start");
+  if constexpr (STAMP) st_t0 = kf_stamp();
   const char* cur = smem;
   init_c(0, cur, mt_of(0));
   init_c(1, cur, mt_of(0));
   constexpr int PD = (VAR & 16) ? 6 : 3, NR = (VAR & 16) ? 8 : 4;  // read distance, operand ring
-  constexpr int BAR = (VAR & 64) ? 0 : 48;  // MFMA step of the per-tile barrier + tile it+2's DMA
+  constexpr int BAR = BAR_OF(VAR);  // MFMA step of the per-tile barrier + tile it+2's DMA
   bf16x8 opr[NR];
 #pragma unroll
   for (int i = 0; i < PD; ++i) opr[i] = opnd(i, cur);
@@ -1338,10 +1359,13 @@ __device__ __forceinline__ void kf_block(
     const int mnext = mt_of(it + 1);
     static_for<0, 64>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
+      if constexpr (STAMP && i == 0) st_prev = kf_stamp();
+      if constexpr (STAMP && (i == 16 || i == 32 || i == 48)) st_ts[i / 16] = kf_stamp();
       if constexpr (i == BAR) {
         // this wave's DMA of tile it+1 landed, the barrier makes every wave's visible and puts
         // everyone past tile it-1, whose slot (it+2) % 3 takes tile it+2
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (STAMP) st_ts[0] = kf_stamp();  // after the barrier
         if constexpr (VAR & 4)
           dma_prep(it + 2, (it + 2) % KF_STAGES);
         else
@@ -1380,7 +1404,30 @@ __device__ __forceinline__ void kf_block(
       __builtin_amdgcn_sched_barrier(0);
       opr[(i + PD) % NR] = nx;
     });
+    if constexpr (STAMP) {
+      // BAR == 0 layout: tile start, barrier done (ts0), 16, 32, 48, end
+      const unsigned long long t = kf_stamp();
+      st_acc[4] += (unsigned)(st_ts[0] - st_prev);
+      st_acc[1] += (unsigned)(st_ts[1] - st_ts[0]);
+      st_acc[2] += (unsigned)(st_ts[2] - st_ts[1]);
+      st_acc[3] += (unsigned)(st_ts[3] - st_ts[2]);
+      st_acc[0] += (unsigned)(t - st_ts[3]);
+    }
     cur = nxt;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      // the order of g_kf_stamp: barrier, 0-15, 16-31, 32-47, 48-63, tiles, blocks, whole block
+      const unsigned long long t = kf_stamp();
+      atomicAdd(&g_kf_stamp[0], (unsigned long long)st_acc[4]);
+      atomicAdd(&g_kf_stamp[1], (unsigned long long)st_acc[1]);
+      atomicAdd(&g_kf_stamp[2], (unsigned long long)st_acc[2]);
+      atomicAdd(&g_kf_stamp[3], (unsigned long long)st_acc[3]);
+      atomicAdd(&g_kf_stamp[4], (unsigned long long)st_acc[0]);
+      atomicAdd(&g_kf_stamp[5], (unsigned long long)total);
+      atomicAdd(&g_kf_stamp[6], 1ull);
+      atomicAdd(&g_kf_stamp[7], t - st_t0);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 #pragma unroll
@@ -1501,7 +1548,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // CU, profiles/r03_flash); bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused
   // register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
-    const int kvar = (flags >> 6) & 127;  // bits 6-12: kf variant (VAR)
+    const int kvar = (flags >> 6) & 255;  // bits 6-13: kf variant (VAR)
     const int nkb_f = (S + KF_BK - 1) / KF_BK;
     const long nkf = (long)((kvar & 32) ? (nkb_f + 1) / 2 : nkb_f) * Hkv * B;
 #define TH_KF_LAUNCH(V_)                                                                                      \
@@ -1513,6 +1560,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
       case 15: TH_KF_LAUNCH(15); break;   // bits 0-3
       case 47: TH_KF_LAUNCH(47); break;   // + paired blocks
       case 111: TH_KF_LAUNCH(111); break;  // + barrier / DMA at the tile start (the default, attention.py)
+      case 239: TH_KF_LAUNCH(239); break;  // 111 + s_memtime stamps (diagnostic, th_kf_stamps)
       default: TH_KF_LAUNCH(0);
     }
 #undef TH_KF_LAUNCH
@@ -1543,6 +1591,15 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
         (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, !(flags & 4));
   TH_CHECK_LAUNCH();
+}
+
+// kf stamp accumulators (VAR bit7 builds): reset = 1 zeroes them, else copies the 8 sums to out
+extern "C" int th_kf_stamps(unsigned long long* out, int reset) {
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_kf_stamp), z, sizeof(z));
+  }
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kf_stamp), 8 * sizeof(unsigned long long));
 }
 
 extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
