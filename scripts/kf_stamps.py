@@ -17,7 +17,7 @@ from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd  # noqa: E40
 
 lib = _lib.load()
 S, Hq, Hkv, D = 4096, 32, 8, 128
-STAMP_FLAGS = 16 | (239 << 6)
+STAMP_FLAGS = 16 | (int(os.environ.get("KF_STAMP_VAR", "239")) << 6)
 buf = (C.c_ulonglong * 8)()
 for B in (4, 8):
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)

@@ -1171,7 +1171,13 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
 // MI355X_MICROARCH 'LDS-DMA piece issue cost'); bit3: the 2-state VALU -> MFMA pad only in front of
 // the MFMAs whose B / C operand a recent gap wrote (0, 16, 32, 33, 48, 49), not all 64; bit4:
 // operands read 6 MFMAs ahead instead of 3; bit6: the barrier and the DMA pieces at the start of
-// the tile, in the gaps of half 0's S|dP chains, which carry no softmax VALU (default: step 48)
+// the tile, in the gaps of half 0's S|dP chains, which carry no softmax VALU (default: step 48);
+// bit8: V fragments negated once per block, so the dP' chain starts from +delta loaded straight
+// into its C registers (no per-tile negation) and yields -dS, whose sign the dK epilogue takes back;
+// bit9 (with bit1): the -inf mask applied only on the tile halves that cross this wave's diagonal
+// (a wave-uniform test), not on every tile; bit10: the init unmasked, and one scalar branch per
+// tile masks the next tile's initial C when it crosses the diagonal; bit11: the paired blocks run by
+// one copy of the block code in a loop (instead of two inlined copies)
 // VAR bit7 (diagnostic builds only): s_memtime stamps per tile phase, summed over all waves into
 // g_kf_stamp = {barrier + DMA wait, MFMA 0-15, 16-31, 32-47, 48-63, wave-tiles, wave-blocks,
 // whole-block cycles}, s_memtime ticks (= shader cycles) summed over waves
@@ -1211,7 +1217,9 @@ __device__ __forceinline__ void kf_block(
 #pragma unroll
     for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
     kf[s] = as_bf(u);
-    vf[s] = as_bf(key < S ? *reinterpret_cast<const ushort8*>(Vb + (long)key * ld + 16 * s + 8 * h) : ushort8(0));
+    ushort8 vv = key < S ? *reinterpret_cast<const ushort8*>(Vb + (long)key * ld + 16 * s + 8 * h) : ushort8(0);
+    if constexpr (VAR & 256) vv ^= (ushort)0x8000;  // -V: dP' = delta - dO V^T, see init_c
+    vf[s] = as_bf(vv);
   }
   f32x16 ak[4], av[4];  // dK^T, dV^T: 128 head dims (4 x 32 accumulator rows) x 32 keys (lanes)
 #pragma unroll
@@ -1244,9 +1252,16 @@ __device__ __forceinline__ void kf_block(
   unsigned d_slot0 = 0, d_img = 0;
   int d_qq0 = 0;
   long d_ldx = ld;
+  int dh_i = 0, dt_i = 0;  // (head, tile) of the next dma_prep, clamped at the last tile
   auto dma_prep = [&](int j, int slot) {
-    j = min(j, total - 1);
-    const int h_i = j / per_head, t_i = j - h_i * per_head;
+    (void)j;
+    const int h_i = __builtin_amdgcn_readfirstlane(dh_i), t_i = __builtin_amdgcn_readfirstlane(dt_i);
+    if (dh_i * per_head + dt_i < total - 1) {
+      if (++dt_i == per_head) {
+        dt_i = 0;
+        ++dh_i;
+      }
+    }
     const int hq = hk * G + h_i;
     d_qq0 = (qt0 + t_i) * C_BQ;
     const bool isq = w < 2;
@@ -1306,7 +1321,7 @@ __device__ __forceinline__ void kf_block(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {  // scalar: packed f32 VALU is an anti-lever beside MFMAs
         cs[kb][4 * g + e] = masked(l[e] * -LOG2E, mt, kb, g, e);
-        cp[kb][4 * g + e] = -dl[e];
+        cp[kb][4 * g + e] = (VAR & 256) ? dl[e] : -dl[e];
       }
     }
   };
@@ -1317,13 +1332,35 @@ __device__ __forceinline__ void kf_block(
     for (int g = 0; g < 4; ++g) {
       lraw[kb][g] = *reinterpret_cast<const float4v*>(rl + 8 * g);
       draw[kb][g] = *reinterpret_cast<const float4v*>(rl + C_BQ + 8 * g);
+      if constexpr (VAR & 256) {  // +delta is the C the -V chain wants: straight from LDS
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cp[kb][4 * g + e] = draw[kb][g][e];
+      }
     }
   };
-  auto conv_c = [&](int kb, int g, int mt) {
+  // diag: some key of this wave exceeds some query of the half (wave-uniform); VAR bit9 masks only then
+  auto conv_c = [&](int kb, int g, int mt, bool diag) {
+    if constexpr (VAR & 1024) {  // unmasked here; mask_fixup() masks the rare diagonal tiles
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      cs[kb][4 * g + e] = masked(lraw[kb][g][e] * -LOG2E, mt, kb, g, e);
-      cp[kb][4 * g + e] = -draw[kb][g][e];
+      for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = lraw[kb][g][e] * -LOG2E;
+    } else if constexpr (VAR & 512) {
+      // a real (scalar) branch: the empty asm keeps hipcc from if-converting it into per-element
+      // selects, which would cost the compares it is meant to skip
+      if (diag) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = masked(lraw[kb][g][e] * -LOG2E, mt, kb, g, e);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = lraw[kb][g][e] * -LOG2E;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = masked(lraw[kb][g][e] * -LOG2E, mt, kb, g, e);
+    }
+    if constexpr (!(VAR & 256)) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cp[kb][4 * g + e] = -draw[kb][g][e];
     }
   };
   // P = exp2(S') (0 where key > query), dS = P dP', packed to the bf16 B operands of the dV / dK
@@ -1338,7 +1375,10 @@ __device__ __forceinline__ void kf_block(
   };
 
   // key - first query of tile t - 4h (causal), or a value no row constant exceeds
-  auto mt_of = [&](int t) { return causal ? key - (qt0 + t % per_head) * C_BQ - 4 * h : -128; };
+  // t = tile index within its head (0 .. per_head-1), kept incrementally (no integer division)
+  auto mt_of = [&](int t) { return causal ? key - (qt0 + t) * C_BQ - 4 * h : -128; };
+  auto diag_of = [&](int t, int kb) { return causal && k0 + 31 > (qt0 + t) * C_BQ + 32 * kb; };
+  int tc = 0;
   constexpr bool STAMP = (VAR & 128) != 0;
   unsigned long long st_t0 = 0, st_prev = 0;
   unsigned st_acc[5] = {0, 0, 0, 0, 0};
@@ -1355,8 +1395,10 @@ __device__ __forceinline__ void kf_block(
   for (int i = 0; i < PD; ++i) opr[i] = opnd(i, cur);
   for (int it = 0; it < total; ++it) {
     const char* nxt = smem + ((it + 1) % KF_STAGES) * KF_TILE;
-    mthr = mt_of(it);  // causal: mask where key > query
-    const int mnext = mt_of(it + 1);
+    const int tn = tc + 1 == per_head ? 0 : tc + 1;
+    mthr = mt_of(tc);  // causal: mask where key > query
+    const int mnext = mt_of(tn);
+    const bool dn0 = diag_of(tn, 0), dn1 = diag_of(tn, 1);
     static_for<0, 64>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (STAMP && i == 0) st_prev = kf_stamp();
@@ -1396,7 +1438,19 @@ __device__ __forceinline__ void kf_block(
       if constexpr (VAR & 1) {
         if constexpr (i == 48) load_c(0, nxt);
         if constexpr (i == 50) load_c(1, nxt);
-        if constexpr (i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext);
+        if constexpr (i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext, i < 58 ? dn0 : dn1);
+        if constexpr ((VAR & 1024) && i == 62) {
+          // one scalar branch per tile, around VALU only (a branch around the asm MFMAs would give
+          // the AGPR accumulators phi copies): -inf where key > query, on the tiles that need it
+          if (dn0 || dn1) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                cs[kb][r] = masked(cs[kb][r], mnext, kb, r >> 2, r & 3);
+          }
+        }
       } else {
         if constexpr (i == 48) init_c(0, nxt, mnext);
         if constexpr (i == 52) init_c(1, nxt, mnext);
@@ -1414,6 +1468,7 @@ __device__ __forceinline__ void kf_block(
       st_acc[0] += (unsigned)(t - st_ts[3]);
     }
     cur = nxt;
+    tc = tn;
   }
   if constexpr (STAMP) {
     if (lane == 0) {
@@ -1437,7 +1492,8 @@ __device__ __forceinline__ void kf_block(
   }
   if (key < S) {
     if (rcos != nullptr) rope_bwd_rows(ak, rcos, rsin, key, h);  // dK rows: rotary backward
-    store_row_t21(dK + b * bs + (long)key * ld + (long)hk * HD, ak, scale, h);
+    // (VAR bit8: the chain computed -dS, so dK^T accumulated -dK^T)
+    store_row_t21(dK + b * bs + (long)key * ld + (long)hk * HD, ak, (VAR & 256) ? -scale : scale, h);
     store_row_t21(dV + b * bs + (long)key * ld + (long)hk * HD, av, 1.f, h);
   }
 }
@@ -1460,9 +1516,21 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
     const int np = (nkb + 1) / 2;
     const int grp = L / np, kb_i = L % np;
     const int b = grp / Hkv, hk = grp % Hkv;
+    const int kb2 = nkb - 1 - kb_i;
+    if constexpr (VAR & 2048) {
+      // one copy of the block code, run once or twice (the two inlined copies below double the
+      // kernel's instruction footprint)
+      const int npass = kb2 != kb_i ? 2 : 1;
+#pragma nounroll
+      for (int pass = 0; pass < npass; ++pass) {
+        if (pass) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        kf_block<VAR>(Q, K, V, dO, LSE, Dl, dK, dV, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale_log2, causal,
+                      rcos, rsin, smem, b, hk, (pass ? kb2 : kb_i) * KF_BK);
+      }
+      return;
+    }
     kf_block<VAR>(Q, K, V, dO, LSE, Dl, dK, dV, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale_log2, causal, rcos,
                   rsin, smem, b, hk, kb_i * KF_BK);
-    const int kb2 = nkb - 1 - kb_i;
     if (kb2 != kb_i) {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // every wave is done with the ring
       kf_block<VAR>(Q, K, V, dO, LSE, Dl, dK, dV, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale_log2, causal,
@@ -1548,7 +1616,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // CU, profiles/r03_flash); bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused
   // register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
-    const int kvar = (flags >> 6) & 255;  // bits 6-13: kf variant (VAR)
+    const int kvar = (flags >> 6) & 4095;  // bits 6-17: kf variant (VAR)
     const int nkb_f = (S + KF_BK - 1) / KF_BK;
     const long nkf = (long)((kvar & 32) ? (nkb_f + 1) / 2 : nkb_f) * Hkv * B;
 #define TH_KF_LAUNCH(V_)                                                                                      \
@@ -1561,6 +1629,12 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
       case 47: TH_KF_LAUNCH(47); break;   // + paired blocks
       case 111: TH_KF_LAUNCH(111); break;  // + barrier / DMA at the tile start (the default, attention.py)
       case 239: TH_KF_LAUNCH(239); break;  // 111 + s_memtime stamps (diagnostic, th_kf_stamps)
+      case 367: TH_KF_LAUNCH(367); break;
+      case 879: TH_KF_LAUNCH(879); break;
+      case 1007: TH_KF_LAUNCH(1007); break;  // 879 + stamps
+      case 1391: TH_KF_LAUNCH(1391); break;  // 367 + mask fix-up on diagonal tiles only
+      case 3439: TH_KF_LAUNCH(3439); break;  // 1391 + one block copy in a loop
+      case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + stamps
       default: TH_KF_LAUNCH(0);
     }
 #undef TH_KF_LAUNCH
