@@ -100,10 +100,11 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 # S % 64 == 0; other lengths keep kh); bit5 register-staged K/V tiles in dQ and the fused dK/dV kernel (the path
 # sequences whose LDS-DMA offsets overflow 32 bits take by themselves).  The 8-wave paired kernels
 # of rounds 2-3 (old bits 6-8) are retired: profiles/r03_flash/retired_kc_kernels.patch
-# Default: kf variant 111 (every bit-0..6 option: lse prefetch, mask in the initial C, per-gap DMA
-# pieces, selective pads, paired key blocks, barrier at the tile start): dK|dV kernel 1072 vs 1133 us
-# for kh at B4 S4096 (profiles/r04_flash/).  0 selects kh.
-KF_DEFAULT_FLAGS = 16 | (111 << 6)
+# Default: kf variant 3439 (flash_attn.hip VAR bits 0-3, 5, 6, 8, 10, 11: lse prefetch, mask in the
+# initial C applied only on diagonal tiles, per-gap DMA pieces, selective pads, paired key blocks,
+# barrier at the tile start, negated V, one block-code copy): whole backward 1.801 vs 1.938 ms for kh
+# at B4 S4096 (profiles/r04_flash/).  0 selects kh.
+KF_DEFAULT_FLAGS = 16 | (3439 << 6)
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", str(KF_DEFAULT_FLAGS)))
 
 

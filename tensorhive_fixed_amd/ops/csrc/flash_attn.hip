@@ -1627,13 +1627,13 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     switch (kvar) {
       case 15: TH_KF_LAUNCH(15); break;   // bits 0-3
       case 47: TH_KF_LAUNCH(47); break;   // + paired blocks
-      case 111: TH_KF_LAUNCH(111); break;  // + barrier / DMA at the tile start (the default, attention.py)
+      case 111: TH_KF_LAUNCH(111); break;  // + barrier / DMA at the tile start
       case 239: TH_KF_LAUNCH(239); break;  // 111 + s_memtime stamps (diagnostic, th_kf_stamps)
       case 367: TH_KF_LAUNCH(367); break;
       case 879: TH_KF_LAUNCH(879); break;
       case 1007: TH_KF_LAUNCH(1007); break;  // 879 + stamps
       case 1391: TH_KF_LAUNCH(1391); break;  // 367 + mask fix-up on diagonal tiles only
-      case 3439: TH_KF_LAUNCH(3439); break;  // 1391 + one block copy in a loop
+      case 3439: TH_KF_LAUNCH(3439); break;  // 1391 + one block copy in a loop (the default, attention.py)
       case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + stamps
       default: TH_KF_LAUNCH(0);
     }
