@@ -1193,6 +1193,27 @@ __device__ __forceinline__ unsigned long long kf_stamp() {
 }
 #define BAR_OF(V) (((V) & 64) ? 0 : 48)
 
+// Phase-2 order of MFMA i (32-63) of a tile: (half, head-dim block d, sub) with sub 0/1 = dV^T from
+// P rows 0-7 / 8-15 of the half and sub 2/3 = dK^T from dS.  Default: d-major (sub 0,1,2,3 per d).
+// VAR bit12: sub-major in the order 0, 2, 1, 3, so a half's elements 8-15 are first needed 8 MFMAs
+// into its phase 2 -- its softmax may then spill into later gaps (kf_softmax_at).
+constexpr int kf_p2_sub(int var, int i) {
+  return (var & 4096) ? (((i - 32) & 15) >> 2 == 0 ? 0 : ((i - 32) & 15) >> 2 == 1 ? 2 : ((i - 32) & 15) >> 2 == 2 ? 1 : 3)
+                      : ((i - 32) & 15) & 3;
+}
+constexpr int kf_p2_d(int var, int i) { return (var & 4096) ? ((i - 32) & 3) : (((i - 32) & 15) >> 2); }
+// softmax element placed in the gap of MFMA i: 16 * half + element, or -1.  Default: half 0 in gaps
+// 16-31, half 1 in 32-47.  VAR bit12: half 0's elements 0-7 in 16-23, 8-15 in the even gaps 24-38;
+// half 1's 0-7 in the odd gaps 33-47, 8-15 in 48-55 (each still done before its first consumer).
+constexpr int kf_softmax_at(int var, int i) {
+  if (!(var & 4096)) return (i >= 16 && i < 48) ? i - 16 : -1;
+  if (i >= 16 && i < 24) return i - 16;
+  if (i >= 24 && i <= 38 && !(i & 1)) return 8 + (i - 24) / 2;
+  if (i >= 33 && i <= 47 && (i & 1)) return 16 + (i - 33) / 2;
+  if (i >= 48 && i < 56) return 24 + (i - 48);
+  return -1;
+}
+
 // one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
 template <int VAR>
 __device__ __forceinline__ void kf_block(
@@ -1302,7 +1323,7 @@ __device__ __forceinline__ void kf_block(
       const int kb = i >> 4, j = (i & 15) >> 1;
       return lds_row((i & 1) ? gs : qs, 32 * kb + c32, 2 * j + h);
     }
-    const int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
+    const int kb = (i - 32) >> 4, d = kf_p2_d(VAR, i), sub = kf_p2_sub(VAR, i);
     return lds_tr(sub < 2 ? gs : qs, 32 * kb + 16 * (sub & 1), 32 * d, lane);
   };
   // -lse2 / -delta of query half kb (accumulator row order) as the S' / dP' chains' initial C
@@ -1418,13 +1439,15 @@ __device__ __forceinline__ void kf_block(
       const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
       __builtin_amdgcn_sched_barrier(0);
       const bf16x8 a = opr[i % NR];
-      constexpr bool pad = !(VAR & 8) || i == 0 || i == 16 || i == 32 || i == 33 || i == 48 || i == 49;
+      // (bit12: the first MFMA of each sub group reads a freshly packed operand)
+      constexpr bool pad = !(VAR & 8) || i == 0 || i == 16 || i == 32 || i == 33 || i == 48 || i == 49 ||
+                           ((VAR & 4096) && i >= 32 && (i & 3) == 0);
       if constexpr (i < 32) {
         constexpr int kb = i >> 4, j = (i & 15) >> 1;
         if constexpr (i & 1) mfma_v<pad>(cp[kb], a, vf[j]);
         else mfma_v<pad>(cs[kb], a, kf[j]);
       } else {
-        constexpr int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
+        constexpr int kb = (i - 32) >> 4, d = kf_p2_d(VAR, i), sub = kf_p2_sub(VAR, i);
         if constexpr (sub < 2) mfma_a<pad>(av[d], a, pp[kb][sub]);
         else mfma_a<pad>(ak[d], a, sp[kb][sub & 1]);
       }
@@ -1434,12 +1457,14 @@ __device__ __forceinline__ void kf_block(
         const int kb = (i >> 4) - 1;
         asm volatile("s_nop 7\n\ts_nop 3" : "+v"(cs[kb]), "+v"(cp[kb]));
       }
-      if constexpr (i >= 16 && i < 48) softmax_elem((i >> 4) - 1, i & 15);
+      if constexpr (kf_softmax_at(VAR, i) >= 0) softmax_elem(kf_softmax_at(VAR, i) >> 4, kf_softmax_at(VAR, i) & 15);
       if constexpr (VAR & 1) {
         if constexpr (i == 48) load_c(0, nxt);
-        if constexpr (i == 50) load_c(1, nxt);
-        if constexpr (i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext, i < 58 ? dn0 : dn1);
-        if constexpr ((VAR & 1024) && i == 62) {
+        // (bit12: half 1's softmax reads cp[1] through gap 55, and bit8 loads delta straight into it)
+        if constexpr (i == ((VAR & 4096) ? 56 : 50)) load_c(1, nxt);
+        constexpr int C0 = (VAR & 4096) ? 56 : 54;  // the init conversion's 8 gaps
+        if constexpr (i >= C0 && i < C0 + 8) conv_c((i - C0) >> 2, (i - C0) & 3, mnext, i < C0 + 4 ? dn0 : dn1);
+        if constexpr ((VAR & 1024) && i == 63) {
           // one scalar branch per tile, around VALU only (a branch around the asm MFMAs would give
           // the AGPR accumulators phi copies): -inf where key > query, on the tiles that need it
           if (dn0 || dn1) {
@@ -1616,7 +1641,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // CU, profiles/r03_flash); bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused
   // register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
-    const int kvar = (flags >> 6) & 4095;  // bits 6-17: kf variant (VAR)
+    const int kvar = (flags >> 6) & 8191;  // bits 6-18: kf variant (VAR)
     const int nkb_f = (S + KF_BK - 1) / KF_BK;
     const long nkf = (long)((kvar & 32) ? (nkb_f + 1) / 2 : nkb_f) * Hkv * B;
 #define TH_KF_LAUNCH(V_)                                                                                      \
@@ -1635,6 +1660,8 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
       case 1391: TH_KF_LAUNCH(1391); break;  // 367 + mask fix-up on diagonal tiles only
       case 3439: TH_KF_LAUNCH(3439); break;  // 1391 + one block copy in a loop (the default, attention.py)
       case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + stamps
+      case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + sub-major phase 2, softmax spread over 16-55
+      case 7663: TH_KF_LAUNCH(7663); break;  // 7535 + stamps
       default: TH_KF_LAUNCH(0);
     }
 #undef TH_KF_LAUNCH
