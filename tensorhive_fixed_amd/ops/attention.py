@@ -94,7 +94,8 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
     return o, lse
 
 
-# launch flags of the backward (th_flash_attn_bwd), A/B aids: bit0 q-major dQ order; bit1 / bit2
+# launch flags of the backward (th_flash_attn_bwd), A/B aids: bit0 q-major dQ order; bit19 dQ tile DMA
+# spread over the first S|dP chain; bit1 / bit2
 # fused dK/dV order / priority; bit3 the fused register-staged dK/dV kernel instead of the paired
 # half-width one; bit4 the one-wave-per-SIMD fused dK|dV kernel with AGPR-pinned accumulators (kf,
 # S % 64 == 0; other lengths keep kh); bit5 register-staged K/V tiles in dQ and the fused dK/dV kernel (the path
@@ -103,8 +104,9 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 # Default: kf variant 3439 (flash_attn.hip VAR bits 0-3, 5, 6, 8, 10, 11: lse prefetch, mask in the
 # initial C applied only on diagonal tiles, per-gap DMA pieces, selective pads, paired key blocks,
 # barrier at the tile start, negated V, one block-code copy): whole backward 1.801 vs 1.938 ms for kh
-# at B4 S4096 (profiles/r04_flash/).  0 selects kh.
-KF_DEFAULT_FLAGS = 16 | (3439 << 6)
+# at B4 S4096 (profiles/r04_flash/).  Bit 19: the dQ kernel's tile DMA spread over its first S|dP
+# chain (708 vs 722 us, 63.4 vs 60.5 % MFMA busy).  0 selects kh and the plain dQ kernel.
+KF_DEFAULT_FLAGS = 16 | (3439 << 6) | (1 << 19)
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", str(KF_DEFAULT_FLAGS)))
 
 

@@ -230,6 +230,19 @@ __device__ __forceinline__ void dma_kv_tile(const ushort* Kb, const ushort* Vb, 
   }
 }
 
+// piece p (0-7) of dma_kv_tile: p >> 1 = the 1 KB slice u, p & 1 = K / V
+__device__ __forceinline__ void dma_kv_piece(const ushort* Kb, const ushort* Vb, long ld, int S, int jt,
+                                             unsigned lds0, int wu, const unsigned (&rc)[4], int p) {
+  const unsigned img = lds0 + (jt & 1) * (2 * 64 * 256) + wu * 4096;
+  const int u = p >> 1;
+  const int row = min(jt * 64 + (int)(rc[u] & 255), S - 1);
+  const unsigned voff = (unsigned)(row * ld + (rc[u] >> 8) * 8) * 2u;
+  if (p & 1)
+    glds16(Vb, voff, img + 64 * 256 + u * 1024);
+  else
+    glds16(Kb, voff, img + u * 1024);
+}
+
 // --------------------------------------------------------------------------------- forward
 #ifndef TH_FA_FWD_DEFAULT
 #define TH_FA_FWD_DEFAULT 15  // PRESCALE + DEFER + DMA-staged DBUF + KVMAJOR: 937 vs 829 TFLOP/s for 11 (B4 S4096, profiles/r01_flash_v3)
@@ -476,7 +489,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 #ifndef TH_DQ_AHEAD
 #define TH_DQ_AHEAD 1  // 0: reads issued right before their MFMA (compiler order)
 #endif
-template <bool KVMAJOR, bool DMA>
+// SPREAD (with DMA): tile j+1's 8 LDS-DMA pieces issued one per MFMA pair of the first S|dP chain
+// (no VALU there) instead of 8 in a row after the barrier -- the kf lesson: a piece costs the issuing
+// wave 60-185 cycles (profiles/r04_flash/)
+template <bool KVMAJOR, bool DMA, bool SPREAD = false>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const ushort* __restrict__ O, const float* __restrict__ LSE,
@@ -559,7 +575,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     char* vs = ks + F_BN * 256;
     if (DMA) {
       wait_dma_barrier();  // tile j landed (every wave's DMA); everyone is past tile j-1
-      if (j + 1 < ntiles) dma_tile(j + 1);
+      if (!SPREAD && j + 1 < ntiles) dma_tile(j + 1);
     } else {
       __syncthreads();
       stage_store<4>(ks, kr, tid);
@@ -571,7 +587,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
       }
     }
     const int kbase = j * F_BN;
-    if (causal && kbase > q0 + 31) continue;
+    // SPREAD: the tile DMA'd this iteration (the last tile re-loads itself into the free image pair,
+    // which nobody reads again: no branch around the pieces)
+    const int jd = min(j + 1, ntiles - 1);
+    if (causal && kbase > q0 + 31) {
+      if (SPREAD) dma_tile(jd);  // this wave skips the tile but still owes its DMA share
+      continue;
+    }
     const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {  // 32-key halves: keeps only one S^T / dP^T pair live
@@ -594,6 +616,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           }
           __builtin_amdgcn_sched_barrier(0);
           sacc = mfma(ka[s & 1], qf[s], sacc);
+          if (SPREAD && kb == 0) dma_kv_piece(Kb, Vb, ld, S, jd, lds0, wu, rc, s);
           pacc = mfma(va[s & 1], gf[s], pacc);
           __builtin_amdgcn_sched_barrier(0);
           ka[s & 1] = kn;
@@ -1624,16 +1647,25 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
   // bit5: register-staged K/V tiles instead of LDS-DMA (also used when 32-bit offsets overflow)
   const bool dq_dma = !(flags & 32) && (long)S * ld * 2 < (1L << 31);
-#define TH_DQ_LAUNCH(KVM, DMA_)                                                                              \
-  fa_bwd_dq_kernel<KVM, DMA_><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, \
-                                                           (const ushort*)dout, (const ushort*)o, lse, delta, (ushort*)dq, \
-                                                           B, S, Hq, \
-                                                           Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, \
-                                                           rcos, rsin)
+  // bit19: the dQ kernel's tile DMA spread over its first S|dP chain (SPREAD)
+  const bool dq_spread = (flags >> 19) & 1;
+#define TH_DQ_LAUNCH(KVM, DMA_, SP_)                                                                         \
+  fa_bwd_dq_kernel<KVM, DMA_, SP_><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, \
+                                                               (const ushort*)dout, (const ushort*)o, lse, delta,     \
+                                                               (ushort*)dq, B, S, Hq, Hkv, ld, bs, ldo, bso, scale,   \
+                                                               scale * LOG2E, causal, rcos, rsin)
   if (flags & 1) {
-    if (dq_dma) TH_DQ_LAUNCH(false, true); else TH_DQ_LAUNCH(false, false);
+    if (dq_dma) {
+      if (dq_spread) TH_DQ_LAUNCH(false, true, true); else TH_DQ_LAUNCH(false, true, false);
+    } else {
+      TH_DQ_LAUNCH(false, false, false);
+    }
   } else {
-    if (dq_dma) TH_DQ_LAUNCH(true, true); else TH_DQ_LAUNCH(true, false);
+    if (dq_dma) {
+      if (dq_spread) TH_DQ_LAUNCH(true, true, true); else TH_DQ_LAUNCH(true, true, false);
+    } else {
+      TH_DQ_LAUNCH(true, false, false);
+    }
   }
 #undef TH_DQ_LAUNCH
   // bit4 (ops/attention.py's default, with a kf variant in bits 6-12): the one-wave-per-SIMD kf
