@@ -29,17 +29,22 @@ for _ in range(9):
         e1.record()
         torch.cuda.synchronize()
         times[f].append(e0.elapsed_time(e1) / 3)
-fwd_t = []
+# forward variants (FA_FWD_VARIANTS, comma list; "d" = the built-in default), interleaved
+fwd_vars = [None if v == "d" else int(v) for v in os.environ.get("FA_FWD_VARIANTS", "d").split(",")]
+fwd_t = {v: [] for v in fwd_vars}
 for _ in range(9):
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(3):
-        flash_fwd(qkv, B, S, Hq, Hkv, D)
-    e1.record()
-    torch.cuda.synchronize()
-    fwd_t.append(e0.elapsed_time(e1) / 3)
-print(json.dumps({"fwd_ms_median": round(statistics.median(fwd_t), 4),
-                  "fwd_tflops": round(4 * B * Hq * S * S * D / 2 / statistics.median(fwd_t) / 1e9, 1)}), flush=True)
+    for v in fwd_vars:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            flash_fwd(qkv, B, S, Hq, Hkv, D, variant=v)
+        e1.record()
+        torch.cuda.synchronize()
+        fwd_t[v].append(e0.elapsed_time(e1) / 3)
+for v in fwd_vars:
+    med = statistics.median(fwd_t[v])
+    print(json.dumps({"fwd_variant": v, "fwd_ms_median": round(med, 4),
+                      "fwd_tflops": round(4 * B * Hq * S * S * D / 2 / med / 1e9, 1)}), flush=True)
 flops = 2.5 * 4 * B * Hq * S * S * D / 2
 for f in flag_sets:
     med = statistics.median(times[f])

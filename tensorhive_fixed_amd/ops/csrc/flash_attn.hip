@@ -244,6 +244,9 @@ __device__ __forceinline__ void dma_kv_piece(const ushort* Kb, const ushort* Vb,
 }
 
 // --------------------------------------------------------------------------------- forward
+#ifndef TH_FA_FWD_SPREAD
+#define TH_FA_FWD_SPREAD 0
+#endif
 #ifndef TH_FA_FWD_DEFAULT
 #define TH_FA_FWD_DEFAULT 15  // PRESCALE + DEFER + DMA-staged DBUF + KVMAJOR: 937 vs 829 TFLOP/s for 11 (B4 S4096, profiles/r01_flash_v3)
 #endif
@@ -270,7 +273,9 @@ __device__ __forceinline__ float half_swap_sum(float x) {
 //   DEFER     skip the O/l rescale while the running max grows by <= F_DEFER_THR (wave-uniform)
 //   DBUF      LDS-DMA staging into double-buffered K/V images: no staging VGPRs / ds_writes, ONE
 //             barrier per key tile instead of two
-template <bool PRESCALE, bool DEFER, bool DBUF, bool KVMAJOR>
+//   SPREAD    (with DBUF) tile j+1's 8 LDS-DMA pieces issued one per MFMA pair of the S chain instead
+//             of 8 in a row after the barrier (profiles/r04_flash/)
+template <bool PRESCALE, bool DEFER, bool DBUF, bool KVMAJOR, bool SPREAD = false>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     ushort* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hkv, long ld,
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     char* vs = ks + F_BN * 256;
     if (DBUF) {
       wait_dma_barrier();  // tile j landed (every wave's DMA); everyone is past tile j-1
-      if (j + 1 < ntiles) dma_kv_tile(Kb, Vb, ld, S, j + 1, lds0, wu, rc);
+      if (!SPREAD && j + 1 < ntiles) dma_kv_tile(Kb, Vb, ld, S, j + 1, lds0, wu, rc);
     } else {
       __syncthreads();
       stage_store<4>(ks, kr, tid);
@@ -345,6 +350,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
       }
     }
     const int kbase = j * F_BN;
+    // SPREAD: the last tile re-loads itself into the free image pair (no branch around the pieces)
+    const int jd = min(j + 1, ntiles - 1);
+    if (SPREAD && causal && kbase > q0 + 31) dma_kv_tile(Kb, Vb, ld, S, jd, lds0, wu, rc);  // skipped: still DMA
     if (!(causal && kbase > q0 + 31)) {  // wave-uniform: tile entirely above the diagonal is skipped
       f32x16 sacc[2] = {s_init, s_init};
       {  // K-row operands are read one k-step ahead of the MFMAs that use them
@@ -359,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
           }
           __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
           sacc[0] = mfma(a0, qf[s], sacc[0]);
+          if (SPREAD) dma_kv_piece(Kb, Vb, ld, S, jd, lds0, wu, rc, s);
           sacc[1] = mfma(a1, qf[s], sacc[1]);
           __builtin_amdgcn_sched_barrier(0);
           a0 = n0;
@@ -1608,8 +1617,16 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   const long nblk = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags: 0 = default variant; 16 + v = explicit v (bit0 PRESCALE, bit1 DEFER, bit2 DBUF,
   // bit3 KVMAJOR block order)
+  // flags bit5 (with 16 + v): SPREAD on the DMA variants (default: TH_FA_FWD_SPREAD)
   int var = flags >= 16 ? (flags & 15) : TH_FA_FWD_DEFAULT;
+  bool spread = flags >= 16 ? ((flags >> 5) & 1) : TH_FA_FWD_SPREAD;
   if ((long)S * ld * 2 >= (1L << 31)) var &= ~4;  // DMA staging uses 32-bit row offsets
+  if (var == 15 && spread) {
+    fa_fwd_kernel<true, true, true, true, true><<<(unsigned)nblk, 256, 0, s>>>(
+        (const ushort*)q, (const ushort*)k, (const ushort*)v, (ushort*)o, lse, B, S, Hq, Hkv, ld, bs, ldo, bso,
+        scale * LOG2E, causal);
+    TH_CHECK_LAUNCH();
+  }
 #define TH_FWD(P, Dd, Db, Km)                                                                      \
   fa_fwd_kernel<P, Dd, Db, Km><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,  \
                                                              (const ushort*)v, (ushort*)o, lse, B,  \

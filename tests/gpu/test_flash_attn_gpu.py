@@ -84,7 +84,7 @@ def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     assert rel < 2e-2, f"dqkv rel err {rel}"
 
 
-@pytest.mark.parametrize("variant", [0, 11, 15], ids=["plain", "prescale_defer", "dma_dbuf"])
+@pytest.mark.parametrize("variant", [0, 11, 15, 31], ids=["plain", "prescale_defer", "dma_dbuf", "dma_spread"])
 def test_flash_fwd_variants_match_reference(variant):
     from tensorhive_fixed_amd.ops.attention import flash_fwd
     torch.manual_seed(2)
