@@ -1,5 +1,5 @@
-"""Where a kf wave's cycles go: run the s_memtime-stamped kf build (VAR 239 = the default 111 + stamps)
-and print cycles per wave per 64-query tile by phase, plus the per-block overhead (prologue: K/V
+"""Where a kf wave's cycles go: run the s_memtime-stamped kf build (VAR 3567 = the default 3439 +
+stamps; KF_STAMP_VAR picks another stamped variant) and print cycles per wave per 64-query tile by phase, plus the per-block overhead (prologue: K/V
 fragments, first two tile DMAs; epilogue: rotary + stores).
 
     python scripts/kf_stamps.py            # B 4 and 8, S 4096, 32/8 heads, d 128, causal
@@ -17,7 +17,7 @@ from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd  # noqa: E40
 
 lib = _lib.load()
 S, Hq, Hkv, D = 4096, 32, 8, 128
-STAMP_FLAGS = 16 | (int(os.environ.get("KF_STAMP_VAR", "239")) << 6)
+STAMP_FLAGS = 16 | (int(os.environ.get("KF_STAMP_VAR", "3567")) << 6)
 buf = (C.c_ulonglong * 8)()
 for B in (4, 8):
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)

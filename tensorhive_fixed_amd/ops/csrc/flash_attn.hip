@@ -1652,6 +1652,10 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 
 // rcos / rsin (the [S][64] rotary tables, or null): the rotary backward of dQ and dK is applied in the
 // dQ and dK|dV kernels' epilogues (default dK|dV kernel only: other flags return -3 with tables given)
+static bool kf_variant_known(int v) {
+  return v == 0 || v == 47 || v == 111 || v == 1391 || v == 3439 || v == 3567 || v == 7535;
+}
+
 static int flash_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
                           const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq,
                           int Hkv, int D, int causal, long ld, long bs, long ldo, long bso, float scale,
@@ -1659,6 +1663,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
   if (rcos != nullptr && ((flags & (8 | 32)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
     return -3;
+  if ((flags & 16) && !kf_variant_known((flags >> 6) & 8191)) return -3;  // before any launch
   if ((flags & 16) && S % C_BQ != 0) flags &= ~16;  // kf assumes whole 64-query tiles: kh instead
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
@@ -1698,20 +1703,17 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
                                                      (const ushort*)dout, lse, delta, (ushort*)dk, (ushort*)dv,   \
                                                      B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, \
                                                      rcos, rsin)
+    // the instantiated variants (profiles/r04_flash/README.md has the measured ones; others are
+    // rejected up front by kf_variant_known)
     switch (kvar) {
-      case 15: TH_KF_LAUNCH(15); break;   // bits 0-3
-      case 47: TH_KF_LAUNCH(47); break;   // + paired blocks
-      case 111: TH_KF_LAUNCH(111); break;  // + barrier / DMA at the tile start
-      case 239: TH_KF_LAUNCH(239); break;  // 111 + s_memtime stamps (diagnostic, th_kf_stamps)
-      case 367: TH_KF_LAUNCH(367); break;
-      case 879: TH_KF_LAUNCH(879); break;
-      case 1007: TH_KF_LAUNCH(1007); break;  // 879 + stamps
-      case 1391: TH_KF_LAUNCH(1391); break;  // 367 + mask fix-up on diagonal tiles only
+      case 0: TH_KF_LAUNCH(0); break;
+      case 47: TH_KF_LAUNCH(47); break;      // bits 0-3 + paired blocks
+      case 111: TH_KF_LAUNCH(111); break;    // + barrier / DMA at the tile start
+      case 1391: TH_KF_LAUNCH(1391); break;  // 111 + negated V + mask fix-up on diagonal tiles only
       case 3439: TH_KF_LAUNCH(3439); break;  // 1391 + one block copy in a loop (the default, attention.py)
-      case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + stamps
-      case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + sub-major phase 2, softmax spread over 16-55
-      case 7663: TH_KF_LAUNCH(7663); break;  // 7535 + stamps
-      default: TH_KF_LAUNCH(0);
+      case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + s_memtime stamps (diagnostic, th_kf_stamps)
+      case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + sub-major phase 2 (measured slower)
+      default: return -3;                    // unreachable: kf_variant_known
     }
 #undef TH_KF_LAUNCH
     TH_CHECK_LAUNCH();
