@@ -1194,25 +1194,27 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
     asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
 
-// VAR bit0: the next tile's lse / delta read from LDS right after the mid-tile barrier and converted
-// four gaps later (default: read and converted in one gap, whose VALU then waits on the reads);
-// bit1: the causal mask applied to the S' chain's initial C (-inf where key > query) in the
-// nearly idle gaps 48-63 instead of to P in the softmax gaps 16-47
-// (exp2(-inf + finite) = 0, and dS = 0 * dP' stays 0); bit2: the 9 DMA pieces of tile it+2 issued
-// one per MFMA gap (48-56) instead of all in gap 48 (a piece costs the issuing wave ~60-185 cycles,
-// MI355X_MICROARCH 'LDS-DMA piece issue cost'); bit3: the 2-state VALU -> MFMA pad only in front of
-// the MFMAs whose B / C operand a recent gap wrote (0, 16, 32, 33, 48, 49), not all 64; bit4:
-// operands read 6 MFMAs ahead instead of 3; bit6: the barrier and the DMA pieces at the start of
-// the tile, in the gaps of half 0's S|dP chains, which carry no softmax VALU (default: step 48);
-// bit8: V fragments negated once per block, so the dP' chain starts from +delta loaded straight
-// into its C registers (no per-tile negation) and yields -dS, whose sign the dK epilogue takes back;
-// bit9 (with bit1): the -inf mask applied only on the tile halves that cross this wave's diagonal
-// (a wave-uniform test), not on every tile; bit10: the init unmasked, and one scalar branch per
-// tile masks the next tile's initial C when it crosses the diagonal; bit11: the paired blocks run by
-// one copy of the block code in a loop (instead of two inlined copies)
-// VAR bit7 (diagnostic builds only): s_memtime stamps per tile phase, summed over all waves into
-// g_kf_stamp = {barrier + DMA wait, MFMA 0-15, 16-31, 32-47, 48-63, wave-tiles, wave-blocks,
-// whole-block cycles}, s_memtime ticks (= shader cycles) summed over waves
+// Variant bits (VAR; launch flags bits 6-18 = VAR; measured in profiles/r04_flash/README.md, the
+// rejected ones -- operands 6 MFMAs ahead, a per-half mask branch, a sub-major phase 2 -- are kept as
+// profiles/r04_flash/rejected_kf_variants.patch):
+//   bit0  the next tile's lse / delta read from LDS right after the barrier, converted 4-8 gaps later
+//   bit1  the causal mask applied to the S' chain's initial C (-inf where key > query) in the nearly
+//         idle gaps 48-63 instead of to P in the softmax gaps (exp2(-inf + finite) = 0, dS = 0 * dP')
+//   bit2  the 9 DMA pieces of tile it+2 issued one per MFMA gap instead of all in one (a piece costs
+//         the issuing wave ~60-185 cycles, MI355X_MICROARCH 'LDS-DMA piece issue cost')
+//   bit3  the 2-state VALU -> MFMA pad only in front of the MFMAs whose B / C a recent gap wrote
+//   bit5  each workgroup takes the key-block pair (i, nkb-1-i): uniform causal work per workgroup
+//   bit6  the barrier and the DMA pieces at the start of the tile, in the gaps of half 0's S|dP
+//         chains, which carry no softmax VALU (default: step 48)
+//   bit7  s_memtime stamps per tile phase (diagnostic build only, scripts/kf_stamps.py)
+//   bit8  V fragments negated once per block, so the dP' chain starts from +delta loaded straight
+//         into its C registers (no per-tile negation) and yields -dS; the dK epilogue takes the sign back
+//   bit10 (with bit1) the init unmasked, and one scalar branch per tile masks the next tile's initial
+//         C when it crosses this wave's diagonal (around VALU only: a branch around the asm MFMAs
+//         gives the AGPR accumulators phi copies)
+//   bit11 the paired blocks run by one copy of the block code in a loop
+// bit7 builds sum their stamps over all waves into g_kf_stamp = {barrier + DMA wait, MFMA 0-15,
+// 16-31, 32-47, 48-63, wave-tiles, wave-blocks, whole-block cycles} (s_memtime ticks = shader cycles)
 __device__ unsigned long long g_kf_stamp[8];
 // one stamp: s_memtime with its own lgkmcnt(0) in the same statement (cdna_hip_programming.md
 // 'In-kernel stamps'; read the SHARES of a stamped build, not its length)
@@ -1224,27 +1226,6 @@ __device__ __forceinline__ unsigned long long kf_stamp() {
   return t;
 }
 #define BAR_OF(V) (((V) & 64) ? 0 : 48)
-
-// Phase-2 order of MFMA i (32-63) of a tile: (half, head-dim block d, sub) with sub 0/1 = dV^T from
-// P rows 0-7 / 8-15 of the half and sub 2/3 = dK^T from dS.  Default: d-major (sub 0,1,2,3 per d).
-// VAR bit12: sub-major in the order 0, 2, 1, 3, so a half's elements 8-15 are first needed 8 MFMAs
-// into its phase 2 -- its softmax may then spill into later gaps (kf_softmax_at).
-constexpr int kf_p2_sub(int var, int i) {
-  return (var & 4096) ? (((i - 32) & 15) >> 2 == 0 ? 0 : ((i - 32) & 15) >> 2 == 1 ? 2 : ((i - 32) & 15) >> 2 == 2 ? 1 : 3)
-                      : ((i - 32) & 15) & 3;
-}
-constexpr int kf_p2_d(int var, int i) { return (var & 4096) ? ((i - 32) & 3) : (((i - 32) & 15) >> 2); }
-// softmax element placed in the gap of MFMA i: 16 * half + element, or -1.  Default: half 0 in gaps
-// 16-31, half 1 in 32-47.  VAR bit12: half 0's elements 0-7 in 16-23, 8-15 in the even gaps 24-38;
-// half 1's 0-7 in the odd gaps 33-47, 8-15 in 48-55 (each still done before its first consumer).
-constexpr int kf_softmax_at(int var, int i) {
-  if (!(var & 4096)) return (i >= 16 && i < 48) ? i - 16 : -1;
-  if (i >= 16 && i < 24) return i - 16;
-  if (i >= 24 && i <= 38 && !(i & 1)) return 8 + (i - 24) / 2;
-  if (i >= 33 && i <= 47 && (i & 1)) return 16 + (i - 33) / 2;
-  if (i >= 48 && i < 56) return 24 + (i - 48);
-  return -1;
-}
 
 // one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
 template <int VAR>
@@ -1355,7 +1336,7 @@ __device__ __forceinline__ void kf_block(
       const int kb = i >> 4, j = (i & 15) >> 1;
       return lds_row((i & 1) ? gs : qs, 32 * kb + c32, 2 * j + h);
     }
-    const int kb = (i - 32) >> 4, d = kf_p2_d(VAR, i), sub = kf_p2_sub(VAR, i);
+    const int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
     return lds_tr(sub < 2 ? gs : qs, 32 * kb + 16 * (sub & 1), 32 * d, lane);
   };
   // -lse2 / -delta of query half kb (accumulator row order) as the S' / dP' chains' initial C
@@ -1391,22 +1372,10 @@ __device__ __forceinline__ void kf_block(
       }
     }
   };
-  // diag: some key of this wave exceeds some query of the half (wave-uniform); VAR bit9 masks only then
-  auto conv_c = [&](int kb, int g, int mt, bool diag) {
-    if constexpr (VAR & 1024) {  // unmasked here; mask_fixup() masks the rare diagonal tiles
+  auto conv_c = [&](int kb, int g, int mt) {
+    if constexpr (VAR & 1024) {  // unmasked here; the fix-up after the conversion masks the rare diagonal tiles
 #pragma unroll
       for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = lraw[kb][g][e] * -LOG2E;
-    } else if constexpr (VAR & 512) {
-      // a real (scalar) branch: the empty asm keeps hipcc from if-converting it into per-element
-      // selects, which would cost the compares it is meant to skip
-      if (diag) {
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = masked(lraw[kb][g][e] * -LOG2E, mt, kb, g, e);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = lraw[kb][g][e] * -LOG2E;
-      }
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = masked(lraw[kb][g][e] * -LOG2E, mt, kb, g, e);
@@ -1441,7 +1410,7 @@ __device__ __forceinline__ void kf_block(
   const char* cur = smem;
   init_c(0, cur, mt_of(0));
   init_c(1, cur, mt_of(0));
-  constexpr int PD = (VAR & 16) ? 6 : 3, NR = (VAR & 16) ? 8 : 4;  // read distance, operand ring
+  constexpr int PD = 3, NR = 4;  // operand read distance (MFMAs), operand ring (6: neutral, profiles/r04_flash)
   constexpr int BAR = BAR_OF(VAR);  // MFMA step of the per-tile barrier + tile it+2's DMA
   bf16x8 opr[NR];
 #pragma unroll
@@ -1471,15 +1440,13 @@ __device__ __forceinline__ void kf_block(
       const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
       __builtin_amdgcn_sched_barrier(0);
       const bf16x8 a = opr[i % NR];
-      // (bit12: the first MFMA of each sub group reads a freshly packed operand)
-      constexpr bool pad = !(VAR & 8) || i == 0 || i == 16 || i == 32 || i == 33 || i == 48 || i == 49 ||
-                           ((VAR & 4096) && i >= 32 && (i & 3) == 0);
+      constexpr bool pad = !(VAR & 8) || i == 0 || i == 16 || i == 32 || i == 33 || i == 48 || i == 49;
       if constexpr (i < 32) {
         constexpr int kb = i >> 4, j = (i & 15) >> 1;
         if constexpr (i & 1) mfma_v<pad>(cp[kb], a, vf[j]);
         else mfma_v<pad>(cs[kb], a, kf[j]);
       } else {
-        constexpr int kb = (i - 32) >> 4, d = kf_p2_d(VAR, i), sub = kf_p2_sub(VAR, i);
+        constexpr int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
         if constexpr (sub < 2) mfma_a<pad>(av[d], a, pp[kb][sub]);
         else mfma_a<pad>(ak[d], a, sp[kb][sub & 1]);
       }
@@ -1489,13 +1456,11 @@ __device__ __forceinline__ void kf_block(
         const int kb = (i >> 4) - 1;
         asm volatile("s_nop 7\n\ts_nop 3" : "+v"(cs[kb]), "+v"(cp[kb]));
       }
-      if constexpr (kf_softmax_at(VAR, i) >= 0) softmax_elem(kf_softmax_at(VAR, i) >> 4, kf_softmax_at(VAR, i) & 15);
+      if constexpr (i >= 16 && i < 48) softmax_elem((i >> 4) - 1, i & 15);
       if constexpr (VAR & 1) {
         if constexpr (i == 48) load_c(0, nxt);
-        // (bit12: half 1's softmax reads cp[1] through gap 55, and bit8 loads delta straight into it)
-        if constexpr (i == ((VAR & 4096) ? 56 : 50)) load_c(1, nxt);
-        constexpr int C0 = (VAR & 4096) ? 56 : 54;  // the init conversion's 8 gaps
-        if constexpr (i >= C0 && i < C0 + 8) conv_c((i - C0) >> 2, (i - C0) & 3, mnext, i < C0 + 4 ? dn0 : dn1);
+        if constexpr (i == 50) load_c(1, nxt);
+        if constexpr (i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext);
         if constexpr ((VAR & 1024) && i == 63) {
           // one scalar branch per tile, around VALU only (a branch around the asm MFMAs would give
           // the AGPR accumulators phi copies): -inf where key > query, on the tiles that need it
@@ -1653,7 +1618,7 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 // rcos / rsin (the [S][64] rotary tables, or null): the rotary backward of dQ and dK is applied in the
 // dQ and dK|dV kernels' epilogues (default dK|dV kernel only: other flags return -3 with tables given)
 static bool kf_variant_known(int v) {
-  return v == 0 || v == 47 || v == 111 || v == 1391 || v == 3439 || v == 3567 || v == 7535;
+  return v == 0 || v == 111 || v == 3439 || v == 3567;
 }
 
 static int flash_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -1707,12 +1672,9 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     // rejected up front by kf_variant_known)
     switch (kvar) {
       case 0: TH_KF_LAUNCH(0); break;
-      case 47: TH_KF_LAUNCH(47); break;      // bits 0-3 + paired blocks
-      case 111: TH_KF_LAUNCH(111); break;    // + barrier / DMA at the tile start
-      case 1391: TH_KF_LAUNCH(1391); break;  // 111 + negated V + mask fix-up on diagonal tiles only
-      case 3439: TH_KF_LAUNCH(3439); break;  // 1391 + one block copy in a loop (the default, attention.py)
+      case 111: TH_KF_LAUNCH(111); break;    // bits 0-3, 5, 6
+      case 3439: TH_KF_LAUNCH(3439); break;  // 111 + bits 8, 10, 11 (the default, attention.py)
       case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + s_memtime stamps (diagnostic, th_kf_stamps)
-      case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + sub-major phase 2 (measured slower)
       default: return -3;                    // unreachable: kf_variant_known
     }
 #undef TH_KF_LAUNCH
