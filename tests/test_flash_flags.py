@@ -1,0 +1,50 @@
+"""CPU checks of the flash-backward launch-flag contract (ops/attention.py <-> ops/csrc/flash_attn.hip).
+
+The default flags select the kf dK|dV kernel variant ``(flags >> 6) & 8191`` and the DMA-spread
+dQ kernel (bit 19). The HIP side rejects variants it does not instantiate (``kf_variant_known``),
+so a default that names a variant missing from the switch would fail every backward on the GPU.
+Catch that here, without a GPU.
+"""
+from __future__ import annotations
+
+import re
+from pathlib import Path
+
+from tensorhive_fixed_amd.ops import attention
+
+SRC = Path(attention.__file__).resolve().parent / "csrc" / "flash_attn.hip"
+
+
+def _known_variants() -> set[int]:
+    text = SRC.read_text()
+    body = re.search(r"static bool kf_variant_known\(int v\) \{(.*?)\}", text, re.S)
+    assert body, "kf_variant_known not found in flash_attn.hip"
+    return {int(x) for x in re.findall(r"v == (\d+)", body.group(1))}
+
+
+def _launched_variants() -> set[int]:
+    text = SRC.read_text()
+    return {int(x) for x in re.findall(r"case (\d+): TH_KF_LAUNCH\(\1\)", text)}
+
+
+def test_default_flags_select_kf_with_rope_fusion_allowed():
+    f = attention.KF_DEFAULT_FLAGS
+    assert f & 16, "bit 4 (kf) must be set"
+    assert not f & (8 | 32), "bits 3 / 5 would disable the fused rotary backward"
+    assert (f >> 19) & 1, "the DMA-spread dQ kernel is part of the default"
+
+
+def test_default_kf_variant_is_instantiated_and_accepted():
+    var = (attention.KF_DEFAULT_FLAGS >> 6) & 8191
+    assert var in _known_variants()
+    assert var in _launched_variants()
+
+
+def test_every_accepted_variant_has_a_launch():
+    assert _known_variants() == _launched_variants()
+
+
+def test_stamped_build_of_the_default_exists():
+    """scripts/kf_stamps.py runs the default variant + bit 7 (stamps)."""
+    var = (attention.KF_DEFAULT_FLAGS >> 6) & 8191
+    assert (var | 128) in _known_variants()
