@@ -1195,8 +1195,8 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
 }
 
 // Variant bits (VAR; launch flags bits 6-18 = VAR; measured in profiles/r04_flash/README.md, the
-// rejected ones -- operands 6 MFMAs ahead, a per-half mask branch, a sub-major phase 2 -- are kept as
-// profiles/r04_flash/rejected_kf_variants.patch):
+// rejected ones -- operands 6 MFMAs ahead, a per-half mask branch, a sub-major phase 2, per-pair
+// bf16 packing -- are kept as profiles/r04_flash/rejected_kf_variants*.patch):
 //   bit0  the next tile's lse / delta read from LDS right after the barrier, converted 4-8 gaps later
 //   bit1  the causal mask applied to the S' chain's initial C (-inf where key > query) in the nearly
 //         idle gaps 48-63 instead of to P in the softmax gaps (exp2(-inf + finite) = 0, dS = 0 * dP')
