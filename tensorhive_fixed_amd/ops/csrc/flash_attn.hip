@@ -1617,6 +1617,8 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 
 // rcos / rsin (the [S][64] rotary tables, or null): the rotary backward of dQ and dK is applied in the
 // dQ and dK|dV kernels' epilogues (default dK|dV kernel only: other flags return -3 with tables given)
+// kf variant: flags bits 6-18
+static int kf_var_of(int flags) { return (flags >> 6) & 8191; }
 static bool kf_variant_known(int v) {
   return v == 0 || v == 111 || v == 3439 || v == 3567;
 }
@@ -1628,7 +1630,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
   if (rcos != nullptr && ((flags & (8 | 32)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
     return -3;
-  if ((flags & 16) && !kf_variant_known((flags >> 6) & 8191)) return -3;  // before any launch
+  if ((flags & 16) && !kf_variant_known(kf_var_of(flags))) return -3;  // before any launch
   if ((flags & 16) && S % C_BQ != 0) flags &= ~16;  // kf assumes whole 64-query tiles: kh instead
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
@@ -1660,7 +1662,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   // CU, profiles/r03_flash); bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused
   // register-staged dK/dV kernel below
   if ((flags & 16) && !(flags & 8) && dq_dma) {  // bit4: the fused one-wave-per-SIMD kernel (kf)
-    const int kvar = (flags >> 6) & 8191;  // bits 6-18: kf variant (VAR)
+    const int kvar = kf_var_of(flags);
     const int nkb_f = (S + KF_BK - 1) / KF_BK;
     const long nkf = (long)((kvar & 32) ? (nkb_f + 1) / 2 : nkb_f) * Hkv * B;
 #define TH_KF_LAUNCH(V_)                                                                                      \
