@@ -1156,16 +1156,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_kh_kernel(
 // dV^T and dK^T of its 32 keys:
 //   * no P exchange through LDS and one barrier per tile (kh: two);
 //   * 4 waves cover 128 keys per staged Q|dO tile (kh: 64), so half the LDS-DMA bytes per MFMA;
-//   * a 3-slot Q|dO ring, DMA two tiles ahead, the barrier in the middle of a tile so the next
-//     tile's first operands are read before this tile's MFMAs run out.
+//   * a 3-slot Q|dO ring with the DMA two tiles ahead, so the next tile's first operands are read
+//     before this tile's MFMAs run out (one barrier per tile, at its start in the default variant).
 // Per 64-query tile a wave issues 64 MFMAs (32x32x16) in one fixed order -- S|dP chains of query
 // half 0 (i = 0-15) and half 1 (16-31), then dV^T|dK^T of half 0 (32-47) and half 1 (48-63) -- with
 // each MFMA's LDS operand read three MFMAs ahead and the softmax-gradient VALU of one half spread
 // one element per MFMA gap over the next 16 MFMAs (half 0 in 16-31, half 1 in 32-47; the next
 // tile's -lse / -delta accumulator init in 48-63).  Every MFMA is inline asm: the S|dP accumulators
 // stay in VGPRs ("+v", no v_accvgpr_read before the exponentials), the dV|dK ones in AGPRs.
-// ring slot: Q | dO | lse | delta as in KC_TILE + 512 B where waves 2-3 drop their copy of the lse /
-// delta load (every wave issues the same DMA sequence: no branch in the loop body)
 // compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N), fully expanded (a 64-step
 // #pragma unroll body exceeds clang's unroll size threshold and stays a runtime loop)
 template <int I, int N, typename F>
@@ -1175,6 +1173,8 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<I + 1, N>(f);
   }
 }
+// ring slot: Q | dO | lse | delta as in KC_TILE + 512 B where waves 2-3 drop their copy of the lse /
+// delta load (every wave issues the same DMA sequence: no branch in the loop body)
 constexpr int KF_BK = 128, KF_STAGES = 3, KF_TILE = KC_TILE + 512, KF_LDS = KF_STAGES * KF_TILE;
 
 // s_nop 1: A/B/C may be fresh VALU results (packed P / dS, the -lse init); hipcc pads nothing in
