@@ -1,4 +1,4 @@
-"""Where a kf wave's cycles go: run the s_memtime-stamped kf build (VAR 3567 = the default 3439 +
+"""Where a kf wave's cycles go: run the s_memtime-stamped kf build (VAR 7663 = the default 7535 +
 stamps; KF_STAMP_VAR picks another stamped variant) and print cycles per wave per 64-query tile by phase, plus the per-block overhead (prologue: K/V
 fragments, first two tile DMAs; epilogue: rotary + stores).
 
@@ -17,7 +17,7 @@ from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd  # noqa: E40
 
 lib = _lib.load()
 S, Hq, Hkv, D = 4096, 32, 8, 128
-STAMP_FLAGS = 16 | (int(os.environ.get("KF_STAMP_VAR", "3567")) << 6)
+STAMP_FLAGS = 16 | (int(os.environ.get("KF_STAMP_VAR", "7663")) << 6) | (1 << 19)
 buf = (C.c_ulonglong * 8)()
 for B in (4, 8):
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)

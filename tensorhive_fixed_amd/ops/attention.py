@@ -107,7 +107,9 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 # barrier at the tile start, negated V, one block-code copy): whole backward 1.801 vs 1.938 ms for kh
 # at B4 S4096 (profiles/r04_flash/).  Bit 19: the dQ kernel's tile DMA spread over its first S|dP
 # chain (708 vs 722 us, 63.4 vs 60.5 % MFMA busy).  0 selects kh and the plain dQ kernel.
-KF_DEFAULT_FLAGS = 16 | (3439 << 6) | (1 << 19)
+# VAR 7535 = 3439 + bit12: the S' chain starts from -lse * log2(e) written by the dQ kernel (no
+# multiply per element in kf): 1023.6 vs 1048.4 us (profiles/r04_flash/kf21_*).
+KF_DEFAULT_FLAGS = 16 | (7535 << 6) | (1 << 19)
 _BWD_FLAGS = int(os.environ.get("TH_FA_BWD_FLAGS", str(KF_DEFAULT_FLAGS)))
 
 
@@ -130,7 +132,8 @@ def flash_bwd(do: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.T
     dqkv = torch.empty_like(qkv)
     # delta = rowsum(dO * O) scratch (dQ is computed by its own query-centric kernel: no f32
     # accumulator, no atomics)
-    delta = torch.empty((B, Hq, S), device=qkv.device, dtype=torch.float32)
+    # [0]: delta, [1]: -lse * log2(e) (written by the dQ kernel for the kf variants that read it)
+    delta = torch.empty((2, B, Hq, S), device=qkv.device, dtype=torch.float32)
     q = qkv.data_ptr()
     k = q + Hq * Dh * 2
     v = k + Hkv * Dh * 2

@@ -501,7 +501,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 // SPREAD (with DMA): tile j+1's 8 LDS-DMA pieces issued one per MFMA pair of the first S|dP chain
 // (no VALU there) instead of 8 in a row after the barrier -- the kf lesson: a piece costs the issuing
 // wave 60-185 cycles (profiles/r04_flash/)
-template <bool KVMAJOR, bool DMA, bool SPREAD = false>
+// L2OUT: also write -lse * log2(e) of each query into Dl[B*Hq*S + ...] (the second half of the
+// delta buffer), so kf VAR bit12 starts its S' chain from it without a multiply per element
+template <bool KVMAJOR, bool DMA, bool SPREAD = false, bool L2OUT = false>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
     const ushort* __restrict__ dO, const ushort* __restrict__ O, const float* __restrict__ LSE,
@@ -543,6 +545,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
   const float lse2 = q < S ? LSE[st + q] * LOG2E : INFINITY;
   const float dsum = half_swap_sum(dpart);
   if (q < S && h == 0) Dl[st + q] = dsum;
+  if (L2OUT && q < S && h == 0) Dl[(long)B * Hq * S + st + q] = -lse2;
   const float dlt = q < S ? dsum : 0.f;
   // Row constants as the initial accumulators (the query is this lane's for the whole kernel): Q is
   // prescaled by softmax_scale * log2(e) once (as the forward's PRESCALE variant does), the S chain
@@ -1213,6 +1216,8 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
 //         C when it crosses this wave's diagonal (around VALU only: a branch around the asm MFMAs
 //         gives the AGPR accumulators phi copies)
 //   bit11 the paired blocks run by one copy of the block code in a loop
+//   bit12 the lse row DMA'd from -lse * log2(e), which the dQ kernel writes (L2OUT) into the second
+//         half of the delta buffer: the S' chain's initial C loads straight from LDS, no multiply
 // bit7 builds sum their stamps over all waves into g_kf_stamp = {barrier + DMA wait, MFMA 0-15,
 // 16-31, 32-47, 48-63, wave-tiles, wave-blocks, whole-block cycles} (s_memtime ticks = shader cycles)
 __device__ unsigned long long g_kf_stamp[8];
@@ -1302,7 +1307,7 @@ __device__ __forceinline__ void kf_block(
     d_base = isq ? Q + b * bs + (long)hq * HD : dO + b * bso + (long)hq * HD;
     d_ldx = isq ? ld : ldo;
     d_slot0 = __builtin_amdgcn_readfirstlane(lds0 + slot * KF_TILE);
-    d_lb = ((w & 1) ? Dl : LSE) + ((long)b * Hq + hq) * S + d_qq0;
+    d_lb = ((w & 1) ? Dl : ((VAR & 4096) ? Dl + (long)B * Hq * S : LSE)) + ((long)b * Hq + hq) * S + d_qq0;
     d_img = d_slot0 + (isq ? 0 : C_BQ * 256) + (w & 1) * 8192;
   };
   auto dma_piece = [&](int u) {
@@ -1354,7 +1359,7 @@ __device__ __forceinline__ void kf_block(
       const float4v dl = *reinterpret_cast<const float4v*>(rd + 8 * g);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {  // scalar: packed f32 VALU is an anti-lever beside MFMAs
-        cs[kb][4 * g + e] = masked(l[e] * -LOG2E, mt, kb, g, e);
+        cs[kb][4 * g + e] = masked((VAR & 4096) ? l[e] : l[e] * -LOG2E, mt, kb, g, e);
         cp[kb][4 * g + e] = (VAR & 256) ? dl[e] : -dl[e];
       }
     }
@@ -1369,6 +1374,10 @@ __device__ __forceinline__ void kf_block(
       if constexpr (VAR & 256) {  // +delta is the C the -V chain wants: straight from LDS
 #pragma unroll
         for (int e = 0; e < 4; ++e) cp[kb][4 * g + e] = draw[kb][g][e];
+      }
+      if constexpr (VAR & 4096) {  // -lse2 precomputed by the dQ kernel: straight from LDS too
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[kb][4 * g + e] = lraw[kb][g][e];
       }
     }
   };
@@ -1460,7 +1469,7 @@ __device__ __forceinline__ void kf_block(
       if constexpr (VAR & 1) {
         if constexpr (i == 48) load_c(0, nxt);
         if constexpr (i == 50) load_c(1, nxt);
-        if constexpr (i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext);
+        if constexpr (!(VAR & 4096) && i >= 54 && i < 62) conv_c((i - 54) >> 2, (i - 54) & 3, mnext);
         if constexpr ((VAR & 1024) && i == 63) {
           // one scalar branch per tile, around VALU only (a branch around the asm MFMAs would give
           // the AGPR accumulators phi copies): -inf where key > query, on the tiles that need it
@@ -1620,7 +1629,7 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 // kf variant: flags bits 6-18
 static int kf_var_of(int flags) { return (flags >> 6) & 8191; }
 static bool kf_variant_known(int v) {
-  return v == 0 || v == 111 || v == 3439 || v == 3567;
+  return v == 0 || v == 111 || v == 3439 || v == 3567 || v == 7535 || v == 7663;
 }
 
 static int flash_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -1638,6 +1647,14 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   const bool dq_dma = !(flags & 32) && (long)S * ld * 2 < (1L << 31);
   // bit19: the dQ kernel's tile DMA spread over its first S|dP chain (SPREAD)
   const bool dq_spread = (flags >> 19) & 1;
+  // kf VAR bit12 reads -lse2 from the dQ kernel (L2OUT) in the second half of the delta buffer
+  const bool dq_l2 = (flags & 16) && !(flags & 8) && dq_dma && (kf_var_of(flags) & 4096);
+  if (dq_l2 && !(dq_spread && !(flags & 1))) return -3;  // instantiated for the default order + spread only
+  if (dq_l2) {
+    fa_bwd_dq_kernel<true, true, true, true><<<(unsigned)nq, 256, 0, s>>>(
+        (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, (const ushort*)o, lse, delta,
+        (ushort*)dq, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, rcos, rsin);
+  } else {
 #define TH_DQ_LAUNCH(KVM, DMA_, SP_)                                                                         \
   fa_bwd_dq_kernel<KVM, DMA_, SP_><<<(unsigned)nq, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, \
                                                                (const ushort*)dout, (const ushort*)o, lse, delta,     \
@@ -1657,6 +1674,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     }
   }
 #undef TH_DQ_LAUNCH
+  }
   // bit4 (ops/attention.py's default, with a kf variant in bits 6-12): the one-wave-per-SIMD kf
   // kernel (profiles/r04_flash); flags 0: the half-width paired dK|dV kernel kh (two workgroups per
   // CU, profiles/r03_flash); bit3, bit5 or 32-bit LDS-DMA offsets that overflow: the fused
@@ -1675,8 +1693,10 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     switch (kvar) {
       case 0: TH_KF_LAUNCH(0); break;
       case 111: TH_KF_LAUNCH(111); break;    // bits 0-3, 5, 6
-      case 3439: TH_KF_LAUNCH(3439); break;  // 111 + bits 8, 10, 11 (the default, attention.py)
+      case 3439: TH_KF_LAUNCH(3439); break;  // 111 + bits 8, 10, 11
       case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + s_memtime stamps (diagnostic, th_kf_stamps)
+      case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + -lse2 from the dQ kernel (bit12; the default, attention.py)
+      case 7663: TH_KF_LAUNCH(7663); break;  // 7535 + stamps
       default: return -3;                    // unreachable: kf_variant_known
     }
 #undef TH_KF_LAUNCH

@@ -13,9 +13,9 @@ def _ref(qkv, B, S, Hq, Hkv, D, causal=True):
     return attention_reference(q, k, v, causal).reshape(B * S, Hq * D)
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 7120, 220112, 744400, 32],
+@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 7120, 220112, 744400, 1006544, 32],
                          ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v111", "kf_v3439", "kf_v3439_dq_spread",
-                              "regstage"])
+                              "kf_v7535_dq_spread", "regstage"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 128, 4, 1), (2, 200, 8, 2), (1, 1024, 32, 8), (1, 64, 2, 2), (3, 192, 4, 2)])
 def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -64,9 +64,9 @@ def test_qkv_attention_with_rope_matches_sdpa_path():
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 7120, 220112, 744400, 32],
+@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 7120, 220112, 744400, 1006544, 32],
                          ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v111", "kf_v3439", "kf_v3439_dq_spread",
-                              "regstage"])
+                              "kf_v7535_dq_spread", "regstage"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 200, 8, 2), (1, 384, 4, 4), (2, 320, 6, 3)])
 def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -95,8 +95,8 @@ def test_flash_fwd_variants_match_reference(variant):
     assert (o.float() - ref).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 220112, 744400],
-                         ids=["kh", "fused_dkv", "kf_one_wave", "kf_v3439", "kf_v3439_dq_spread"])
+@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 220112, 744400, 1006544],
+                         ids=["kh", "fused_dkv", "kf_one_wave", "kf_v3439", "kf_v3439_dq_spread", "kf_v7535_dq_spread"])
 @pytest.mark.parametrize("S,Hq,Hkv", [(4096, 32, 8), (8192, 8, 2)], ids=["S4096_bench_heads", "S8192_model_max"])
 def test_flash_long_sequences_match_fp32(S, Hq, Hkv, bwd_flags):
     """The training shapes: S = 4096 (the bench) with Llama-3-8B's 32/8 heads, and S = 8192 (the
@@ -131,7 +131,8 @@ def test_flash_long_sequences_match_fp32(S, Hq, Hkv, bwd_flags):
         del x, q, k, v, s, p, og, g
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 16, 220112, 744400], ids=["kh", "kf_one_wave", "kf_v3439", "kf_v3439_dq_spread"])
+@pytest.mark.parametrize("bwd_flags", [0, 16, 220112, 744400, 1006544],
+                         ids=["kh", "kf_one_wave", "kf_v3439", "kf_v3439_dq_spread", "kf_v7535_dq_spread"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 8, 2), (2, 200, 4, 4), (1, 4096, 32, 8)])
 def test_rotary_backward_in_the_kernels_matches_the_separate_pass(B, S, Hq, Hkv, bwd_flags):
     """The rotary backward folded into the dQ / dK epilogues gives the dqkv of the flash backward
