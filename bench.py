@@ -64,6 +64,10 @@ def main() -> int:
     ap.add_argument("--daemon-bench", type=int, default=1,
                     help="rank 0 also measures the daemon's dashboard poll latency after the timed steps")
     args = ap.parse_args()
+    # bench-only diagnostics: RCCL's INIT log to a per-rank file summarised in the JSON line, and
+    # the exposed-communication wait spans (both off for ordinary training jobs)
+    os.environ.setdefault("TH_RCCL_INIT_LOG", "1")
+    os.environ.setdefault("TH_COMM_TIMING", "1")
 
     from tensorhive_fixed_amd.utils.blas_env import refuse_unsafe_blas_workspace
 

@@ -2,7 +2,10 @@
 stamps; KF_STAMP_VAR picks another stamped variant) and print cycles per wave per 64-query tile by phase, plus the per-block overhead (prologue: K/V
 fragments, first two tile DMAs; epilogue: rotary + stores).
 
-    python scripts/kf_stamps.py            # B 4 and 8, S 4096, 32/8 heads, d 128, causal
+    bash scripts/build_variant_lib.sh kf_diag -DTH_KF_DIAG=1     # the diagnostic library
+    TH_KERNEL_LIB=ab_libs/kf_diag.so python scripts/kf_stamps.py  # B 4 and 8, S 4096, 32/8 heads, d 128
+
+The production libthk.so has no stamped variants and no ``th_kf_stamps`` (flash_attn.hip TH_KF_DIAG).
 """
 import ctypes as C
 import json
@@ -16,6 +19,10 @@ from tensorhive_fixed_amd.ops import _lib  # noqa: E402
 from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd  # noqa: E402
 
 lib = _lib.load()
+if not hasattr(lib, "th_kf_stamps"):
+    sys.exit(f"{_lib.library_path()} is a production build: set TH_KERNEL_LIB to the TH_KF_DIAG library")
+lib.th_kf_stamps.argtypes = [C.c_void_p, C.c_int]
+lib.th_kf_stamps.restype = C.c_int
 S, Hq, Hkv, D = 4096, 32, 8, 128
 STAMP_FLAGS = 16 | (int(os.environ.get("KF_STAMP_VAR", "7663")) << 6) | (1 << 19)
 buf = (C.c_ulonglong * 8)()

@@ -10,7 +10,8 @@
 // brace expansion ({a,b}, {1..3}), and JSON documents
 // (TF_CONFIG), are single-quoted.  isOneShellWord mirrors _is_one_shell_word line for line.
 export function isOneShellWord(v) {
-  let words = 0, inWord = false, quote = "", brace = 0, i = 0;
+  // braces: one entry per open '{' -- whether that level saw an unquoted ',' or '..'
+  let words = 0, inWord = false, quote = "", braces = [], i = 0;
   while (i < v.length) {
     const c = v[i];
     if (quote === "'") {
@@ -19,7 +20,7 @@ export function isOneShellWord(v) {
       if (c === "\\") i += 1;
       else if (c === '"') quote = "";
     } else if (" \t\n".includes(c)) {
-      inWord = false; brace = 0;
+      inWord = false; braces = [];
     } else if (";&|<>()".includes(c)) {
       return false;
     } else {
@@ -29,11 +30,10 @@ export function isOneShellWord(v) {
       }
       if (c === "\\") i += 1;
       else if (c === "'" || c === '"') quote = c;
-      else if (c === "{") brace = 1;
-      else if (brace && (c === "," || (c === "." && v.slice(i + 1, i + 2) === "."))) brace = 2;
-      else if (c === "}") {
-        if (brace === 2) return false;
-        brace = 0;
+      else if (c === "{") braces.push(false);
+      else if (braces.length && (c === "," || (c === "." && v.slice(i + 1, i + 2) === "."))) braces[braces.length - 1] = true;
+      else if (c === "}" && braces.length) {
+        if (braces.pop()) return false;
       }
     }
     i += 1;

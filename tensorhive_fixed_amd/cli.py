@@ -123,18 +123,20 @@ def main(ctx, version, log_level, log_dir, config_dir, json_logs):
 
 
 def refuse_insecure_secret(cfg) -> None:
-    """Exit when the JWT signing key is empty or public (anyone reaching :1111 could mint an admin
-    token and run jobs as any user); ``TENSORHIVE_ALLOW_INSECURE_SECRET=1`` overrides (tests)."""
-    from .config import ALLOW_INSECURE_ENV, insecure_secret_allowed, secret_is_insecure
+    """Exit when the JWT signing key is empty, public or shorter than 32 characters (anyone reaching
+    :1111 could mint -- or brute-force the key of -- an admin token and run jobs as any user);
+    ``TENSORHIVE_ALLOW_INSECURE_SECRET=1`` overrides (tests)."""
+    from .config import ALLOW_INSECURE_ENV, MIN_SECRET_LEN, insecure_secret_allowed, secret_is_insecure
 
     if not secret_is_insecure(cfg.auth.secret_key):
         return
     if insecure_secret_allowed():
-        logging.getLogger(__name__).warning("[auth] secret_key is public; allowed by %s", ALLOW_INSECURE_ENV)
+        logging.getLogger(__name__).warning("[auth] secret_key is insecure; allowed by %s", ALLOW_INSECURE_ENV)
         return
     raise click.ClickException(
-        f"[auth] secret_key in {cfg.directory / 'main_config.ini'} is empty or the public default "
-        "'jwt-some-secret'; run `tensorhive init` (writes a random key) or set one yourself")
+        f"[auth] secret_key in {cfg.directory / 'main_config.ini'} is empty, the public default "
+        f"'jwt-some-secret' or shorter than {MIN_SECRET_LEN} characters; run `tensorhive init` "
+        "(writes a random key) or set a long random one yourself")
 
 
 def run_daemon(block: bool = True):

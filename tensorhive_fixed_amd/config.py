@@ -50,8 +50,18 @@ ALLOW_INSECURE_ENV = "TENSORHIVE_ALLOW_INSECURE_SECRET"
 _SECRET_LINE = re.compile(r"^(\s*secret_key\s*=)[ \t]*(.*)$", re.M)
 
 
-def secret_is_insecure(secret: str | None) -> bool:
+MIN_SECRET_LEN = 32  # characters; new_secret() writes 64 hex digits (256 bits)
+
+
+def secret_is_public(secret: str | None) -> bool:
+    """Empty or a key published with the reference: replaced by a random one on startup."""
     return (secret or "").strip() in INSECURE_SECRETS
+
+
+def secret_is_insecure(secret: str | None) -> bool:
+    """Public, or too short to resist an offline guess of the HS256 key (a one-character key
+    would be found from any token in microseconds): the daemon refuses to start with it."""
+    return secret_is_public(secret) or len((secret or "").strip()) < MIN_SECRET_LEN
 
 
 def insecure_secret_allowed() -> bool:
@@ -77,8 +87,8 @@ def ensure_secret_key(path: Path | str) -> bool:
         if cp.has_option("auth", k):
             current = cp.get("auth", k)
             break
-    if current is not None and not secret_is_insecure(current):
-        return False
+    if current is not None and not secret_is_public(current):
+        return False  # the operator's own key: kept (refused at startup if it is too short)
     key = new_secret()
     if current is not None and _SECRET_LINE.search(text):
         text = _SECRET_LINE.sub(lambda m: f"{m.group(1)} {key}", text, count=1)

@@ -1,0 +1,190 @@
+"""Task attribution that cannot be forged (round-4 verdict item 1).
+
+A GPU process *claims* a TensorHive task through ``TENSORHIVE_TASK_ID`` in its environment, which
+anybody can set.  The claim is accepted only when the process really belongs to that task's
+``th-run`` session on that node:
+
+* its uid is the uid the task runs as (``uid``/``user`` in th-run's state file), **and**
+* its session id is the task's session (``sid``: th-run's first child called ``setsid``; every
+  process the task forks stays in it), **or** its parent chain reaches the task's ``th-run``
+  monitor (a rank that called ``setsid`` itself).
+
+A process started outside the session cannot join it (``setsid``/``setpgid`` only leave or move
+within a session), and a user cannot take another uid, so the check holds against a process that
+copies a victim's task id.  A claim that fails is dropped: the process keeps ``claimed_task_id``
+and is judged by its UNIX owner, exactly like the reference, whose enforcer knew no tasks at all
+(``tensorhive/core/services/ProtectionService.py:97-99``, owner from ``ps -o user`` in
+``tensorhive/core/monitors/GPUMonitor.py:94-107``).
+
+The session facts come from th-run itself: the spawn command prints the new session's state in the
+same round trip (``task_nursery.spawn``), every ``th-run ls`` refreshes them
+(``task_nursery.running``), and a claim for a task the registry has not seen (a daemon restarted
+under a running task) triggers one rate-limited ``th-run ls`` of that task's owner on that node
+before it is judged.
+
+:meth:`Attestor.attest_entry` runs in the monitoring service before a sample is published, so every
+consumer -- :class:`~.services.ProtectionService`, the queue's eviction check
+(``JobSchedulingService.sync_running_from_queue``), the in-task HBM counters (``core/hbm.py``) and
+the ``/nodes`` API -- sees attested task ids only.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+
+from . import hbm
+
+log = logging.getLogger(__name__)
+
+SESSION_PREFIX = "tensorhive_task_"
+
+
+def _int(v) -> int | None:
+    try:
+        return int(v)
+    except (TypeError, ValueError):
+        return None
+
+
+def task_id_of_session(name: str) -> str | None:
+    name = str(name or "")
+    return name[len(SESSION_PREFIX):] if name.startswith(SESSION_PREFIX) else None
+
+
+class SessionRegistry:
+    """``(host, task id) -> th-run session facts`` (sid, uid, user, monitor pid, pids), fed by
+    every th-run listing the daemon reads."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._d: dict[tuple[str, str], dict] = {}
+
+    def record(self, host: str, sess: dict, listed_as: str | None = None) -> None:
+        """``listed_as``: the login whose th-run state this session came from."""
+        tid = task_id_of_session(sess.get("name"))
+        if tid is None:
+            return
+        rec = {"sid": _int(sess.get("sid")), "uid": _int(sess.get("uid")), "user": sess.get("user") or None,
+               "monitor_pid": _int(sess.get("monitor_pid")), "pid": _int(sess.get("pid")),
+               "listed_as": listed_as, "seen": time.monotonic()}
+        with self._lock:
+            self._d[(host, tid)] = rec
+
+    def replace_listing(self, host: str, user: str | None, sessions: list[dict]) -> None:
+        """A complete live listing of the sessions ``user`` sees on ``host``: record them and forget
+        the sessions of that listing that are no longer live (their sid may be reused later)."""
+        live = set()
+        for s in sessions:
+            self.record(host, s, listed_as=user)
+            tid = task_id_of_session(s.get("name"))
+            if tid is not None:
+                live.add(tid)
+        if user is None:
+            return
+        with self._lock:
+            for (h, tid), rec in list(self._d.items()):
+                if h == host and rec.get("listed_as") == user and tid not in live:
+                    del self._d[(h, tid)]
+
+    def get(self, host: str, task_id) -> dict | None:
+        with self._lock:
+            r = self._d.get((host, str(task_id)))
+            return dict(r) if r else None
+
+    def forget(self, host: str, task_id) -> None:
+        with self._lock:
+            self._d.pop((host, str(task_id)), None)
+
+    def clear(self) -> None:
+        with self._lock:
+            self._d.clear()
+
+
+REGISTRY = SessionRegistry()
+
+
+def check(proc: dict, sess: dict | None) -> str | None:
+    """Why ``proc``'s task claim does not hold against the task's session ``sess`` (None = holds)."""
+    if sess is None:
+        return "no th-run session of that task on this node"
+    puid, suid = _int(proc.get("uid")), sess.get("uid")
+    if puid is not None and puid >= 0 and suid is not None:
+        if puid != suid:
+            return f"uid {puid} is not the task's uid {suid}"
+    elif proc.get("owner") and sess.get("user"):
+        if proc["owner"] != sess["user"]:
+            return f"owner {proc['owner']} is not the task's user {sess['user']}"
+    else:
+        return "the process's uid is unknown"
+    psid, ssid = _int(proc.get("sid")), sess.get("sid")
+    if psid is not None and psid > 0 and ssid is not None and psid == ssid:
+        return None
+    mon = sess.get("monitor_pid")
+    if mon is not None and mon in {_int(a) for a in (proc.get("ancestors") or [])}:
+        return None
+    return "not in the task's th-run session"
+
+
+class Attestor:
+    """Replaces every unverifiable ``task_id`` of an infrastructure entry before it is published.
+
+    ``lookup(host, task_id)`` (optional) refreshes the registry for a task it has not seen, at most
+    once per ``refetch_s`` per (host, task): the daemon's implementation lists the task owner's
+    sessions on that node (``task_nursery.running``), which also records them."""
+
+    def __init__(self, registry: SessionRegistry = REGISTRY, lookup=None, refetch_s: float = 5.0):
+        self.registry = registry
+        self.lookup = lookup
+        self.refetch_s = refetch_s
+        self._fetched: dict[tuple[str, str], float] = {}
+        self._warned: dict[tuple[str, int, str], float] = {}
+        self.rejected = 0
+
+    def _session(self, host: str, tid: str) -> dict | None:
+        sess = self.registry.get(host, tid)
+        if sess is None and self.lookup is not None:
+            k = (host, tid)
+            now = time.monotonic()
+            if now - self._fetched.get(k, -1e9) >= self.refetch_s:
+                self._fetched[k] = now
+                try:
+                    self.lookup(host, tid)
+                except Exception as e:  # noqa: BLE001 -- unreachable node: the claim stays unverified
+                    log.debug("attribution: session lookup of task %s on %s failed: %s", tid, host, e)
+                sess = self.registry.get(host, tid)
+        return sess
+
+    def verify(self, host: str, proc: dict) -> bool:
+        tid = proc.get("task_id")
+        if tid in (None, ""):
+            return False
+        why = check(proc, self._session(host, str(tid)))
+        if why is None:
+            return True
+        self.rejected += 1
+        k = (host, _int(proc.get("pid")) or 0, str(tid))
+        now = time.monotonic()
+        if now - self._warned.get(k, -1e9) > 60.0:
+            self._warned[k] = now
+            log.warning("attribution: pid %s on %s (owner %s) claims task %s: rejected, %s", proc.get("pid"), host,
+                        proc.get("owner"), tid, why)
+        return False
+
+    def attest_entry(self, host: str, entry: dict | None) -> dict | None:
+        """In place: keep each process's ``task_id`` only if it verifies (else move it to
+        ``claimed_task_id``), then derive the in-task HBM metrics from the attested processes."""
+        if not entry:
+            return entry
+        for g in (entry.get("GPU") or {}).values():
+            if not g:
+                continue
+            for p in g.get("processes") or []:
+                tid = p.get("task_id")
+                if tid in (None, ""):
+                    continue
+                if not self.verify(host, p):
+                    p["claimed_task_id"] = str(tid)
+                    p["task_id"] = None
+        hbm.finalize_entry(entry)
+        return entry

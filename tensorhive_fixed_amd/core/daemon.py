@@ -47,7 +47,12 @@ class Daemon:
         from . import task_nursery
 
         task_nursery.use_transports(self.transports)
-        self.infrastructure = InfrastructureStore(list(nodes))
+        from .attribution import REGISTRY, Attestor
+
+        # every sample is attested as it is published: a process's TENSORHIVE_TASK_ID counts only
+        # inside that task's th-run session and uid (core/attribution.py)
+        self.attestor = Attestor(REGISTRY, lookup=self.lookup_task_sessions)
+        self.infrastructure = InfrastructureStore(list(nodes), attest=self.attestor.attest_entry)
         if backends is None:
             am = self.cfg.amd_monitor
             shared: dict = {}
@@ -136,6 +141,25 @@ class Daemon:
 
         if task_nursery._transports is self.transports:
             task_nursery.use_transports(None)
+
+    def lookup_task_sessions(self, host: str, task_id: str) -> None:
+        """Refresh the attestation registry for a claimed task it has not seen: list the task
+        owner's th-run sessions on ``host`` (which records them).  Claims naming no task of that
+        host cost no round trip."""
+        from ..database import db_session
+        from ..models.orm import Task
+        from . import task_nursery
+
+        try:
+            t = Task.query.filter(Task.id == int(task_id)).first()
+            user = t.job.user.username if t is not None and t.job is not None and t.job.user else None
+            if user is None or t.hostname != host:
+                return
+        except (ValueError, TypeError):
+            return
+        finally:
+            db_session.remove()
+        task_nursery.running(host, user)
 
     def wake(self, reason: str = "") -> None:
         """Event-driven wake-up of the job scheduler (enqueue, reservation change, job stop, and

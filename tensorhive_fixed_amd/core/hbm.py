@@ -9,7 +9,10 @@ do this -- on this stack the TCC request counters only count the counting proces
 
 :func:`read_rates` returns ``{bdf: {"hbm_read": GB/s, "hbm_write": GB/s, "pids": [...]}}`` over
 the live, fresh files whose owner owns the pid; files of dead processes are removed.
-:func:`metrics_for` keeps only pids libthsmi lists on that GPU as th-run task processes.  GPUs
+:func:`metrics_for` keeps only pids libthsmi lists on that GPU as th-run task processes.  On a
+node, the task ids are the processes' own claims; the daemon re-derives the metrics after
+``core/attribution.py`` has attested every claim (:func:`finalize_entry`), so a process that
+forges a task id cannot get its counts -- or its silence -- accepted.  GPUs
 without a counting task keep libthsmi's ``mem_activity_acc``-based ``hbm_bw`` estimate; GPUs
 where only some processes are counted say ``partial`` (``hbm_bw_source`` says which).
 """
@@ -19,8 +22,8 @@ import glob
 import json
 import logging
 import os
+import stat
 import time
-from pathlib import Path
 
 log = logging.getLogger(__name__)
 
@@ -57,6 +60,35 @@ def _proc_uid(pid: int) -> int | None:
         return None
 
 
+MAX_FILE_BYTES = 64 << 10
+
+
+def _read_small_regular(path: str) -> tuple[os.stat_result, bytes]:
+    """Read a counter file that any local user could have planted: never follow a symlink, never
+    block on a FIFO, only a regular file of at most ``MAX_FILE_BYTES``; the stat (owner) is the
+    one of the file actually read."""
+    fd = os.open(path, os.O_RDONLY | os.O_NOFOLLOW | os.O_NONBLOCK | getattr(os, "O_CLOEXEC", 0))
+    try:
+        st = os.fstat(fd)
+        if not stat.S_ISREG(st.st_mode):
+            raise OSError(f"{path}: not a regular file")
+        if st.st_size > MAX_FILE_BYTES:
+            raise OSError(f"{path}: {st.st_size} bytes")
+        chunks, left = [], MAX_FILE_BYTES + 1
+        while left > 0:
+            b = os.read(fd, left)
+            if not b:
+                break
+            chunks.append(b)
+            left -= len(b)
+        data = b"".join(chunks)
+        if len(data) > MAX_FILE_BYTES:
+            raise OSError(f"{path}: grew past the cap")
+        return st, data
+    finally:
+        os.close(fd)
+
+
 def read_rates(pattern: str = SHM_GLOB, max_age_s: float = 5.0, now: float | None = None,
                cleanup: bool = True) -> dict[str, dict]:
     """``{bdf: {"hbm_read", "hbm_write", "pids", "by_pid": {pid: (rd GB/s, wr GB/s)}}}`` over the
@@ -68,10 +100,10 @@ def read_rates(pattern: str = SHM_GLOB, max_age_s: float = 5.0, now: float | Non
     out: dict[str, dict] = {}
     for f in glob.glob(pattern):
         try:
-            st = os.stat(f)
-            doc = json.loads(Path(f).read_text())
+            st, raw = _read_small_regular(f)
+            doc = json.loads(raw)
             pid = int(doc.get("pid") or 0)
-        except (OSError, ValueError, TypeError):
+        except (OSError, ValueError, TypeError, AttributeError):
             continue
         if pid <= 0:
             continue
@@ -153,3 +185,36 @@ def metrics_for(gpus: list[dict], rates: dict[str, dict]) -> dict[int, dict]:
             m["hbm_bw_source"] = {"value": "counters", "unit": ""}
         out[g["index"]] = m
     return out
+
+
+_DERIVED = ("hbm_read", "hbm_write", "hbm_counted", "hbm_bw_source", "hbm_uncounted_pids")
+
+
+def raw_counts(rates: dict[str, dict], bdf) -> dict | None:
+    """The per-pid counted rates of one GPU in wire form (``{"<pid>": [rd, wr]}``), or None."""
+    r = rates.get(bdf)
+    if not r:
+        return None
+    by_pid = r.get("by_pid") or {}
+    return {str(pid): [round(v[0], 3), round(v[1], 3)] for pid, v in by_pid.items()}
+
+
+def finalize_entry(entry: dict) -> dict:
+    """Re-derive the counter-based HBM metrics of an infrastructure entry from its raw per-pid
+    counts (``_hbm``, attached by ``telemetry.apply_task_hbm``) and the CURRENT -- attested -- task
+    ids of its processes, then drop the raw counts.  GPUs without raw counts are left alone."""
+    for g in ((entry or {}).get("GPU") or {}).values():
+        if not g or "_hbm" not in g:
+            continue
+        raw = g.pop("_hbm") or {}
+        m = g.setdefault("metrics", {})
+        for k in _DERIVED:
+            m.pop(k, None)
+        if raw.get("est") is not None or "hbm_bw" in m:
+            m["hbm_bw"] = {"value": raw.get("est"), "unit": "GB/s"}
+        counts = raw.get("counts") or {}
+        rates = {g.get("bdf"): {"by_pid": {int(p): (float(v[0]), float(v[1])) for p, v in counts.items()},
+                                "pids": [int(p) for p in counts]}} if counts else {}
+        got = metrics_for([g], rates).get(g.get("index")) if rates else None
+        m.update(got or {"hbm_bw_source": {"value": "umc_activity", "unit": ""}})
+    return entry

@@ -16,9 +16,12 @@ Shape (the wire contract of ``/nodes/*``)::
 from __future__ import annotations
 
 import copy
+import logging
 import threading
 import time
 from dataclasses import dataclass, field
+
+log = logging.getLogger(__name__)
 
 IGNORED_PROCESSES = ("Xorg", "/usr/lib/xorg/Xorg", "/usr/bin/X", "X", "gnome-shell", "-")
 
@@ -35,13 +38,26 @@ class Snapshot:
 
 
 class InfrastructureStore:
-    def __init__(self, hosts):
+    """``attest(host, entry)`` (the daemon's ``core/attribution.Attestor``) runs on every entry
+    before it is published: consumers only ever see attested task ids."""
+
+    def __init__(self, hosts, attest=None):
         self._lock = threading.Lock()  # serialises writers only
         self._snap = Snapshot(0, {h: {} for h in hosts}, {})
         self._listeners: list = []
+        self.attest = attest
 
     # ------------------------------------------------------------------ writers
     def publish(self, host: str, entry: dict, sampled_at: float | None = None) -> Snapshot:
+        if self.attest is not None and entry:
+            try:
+                self.attest(host, entry)
+            except Exception:  # noqa: BLE001 -- never publish unattested claims
+                log.exception("attestation of %s failed; dropping its task claims", host)
+                for g in (entry.get("GPU") or {}).values():
+                    for p in (g or {}).get("processes") or []:
+                        if p.get("task_id") not in (None, ""):
+                            p["claimed_task_id"], p["task_id"] = str(p["task_id"]), None
         with self._lock:
             old = self._snap
             data = dict(old.data)

@@ -6,9 +6,10 @@ statistics (p50/p99 exposed at ``/api/metrics/internal``).
 * :class:`MonitoringService` -- samples every host's telemetry backend (in parallel) at
   ``update_interval`` (sub-second for the native sampler) and publishes immutable snapshots.
 * :class:`ProtectionService` -- foreign processes on reserved GPUs (level 1) or on any
-  GPU without the owner's reservation (level 2, strict) -> violation handlers.  Processes
-  launched by a TensorHive task of the reservation owner (``TENSORHIVE_TASK_ID``) are never
-  violations.
+  GPU without the owner's reservation (level 2, strict) -> violation handlers.  Processes of a
+  TensorHive task of the reservation owner are never violations -- a task id counts only after
+  ``core/attribution.py`` attested it (the process is in that task's th-run session and runs as
+  its uid; the infrastructure store attests every sample it publishes).
 * :class:`UsageLoggingService` -- per-reservation JSON time series; on expiry stores rounded
   averages on the reservation (+ extra MI355X metric averages in the JSON summary).
 * :class:`JobSchedulingService` -- scheduled start/stop, queued gang scheduling and eviction of

@@ -12,7 +12,9 @@ Public functions keep the reference's shape:
   * :func:`fetch_log` -- ``~/TensorHiveLogs/task_<id>.log`` (whole file or tail).
 Names (``tensorhive_task_<id>``) and log paths are unchanged.  Every task gets
 ``TENSORHIVE_TASK_ID=<id>`` in its environment, which the telemetry uses to attribute GPU
-processes to tasks exactly.  If ``th-run`` is not installed on a remote node, a ``setsid`` +
+processes to tasks -- a claim the daemon accepts only for processes of that task's th-run session
+running as its uid (``core/attribution.py``, fed by the session state :func:`spawn` and
+:func:`running` read).  If ``th-run`` is not installed on a remote node, a ``setsid`` +
 ``tee`` shell fallback keeps spawn/kill/log working.
 """
 from __future__ import annotations
@@ -22,7 +24,7 @@ import logging
 import shlex
 
 from ..config import get_config
-from . import ssh
+from . import attribution, ssh
 from .transport import Result, TransportManager
 
 log = logging.getLogger(__name__)
@@ -87,7 +89,10 @@ def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | No
     policy = ""
     if max_restarts and int(max_restarts) > 0:  # th-run restarts a failed run (the fallback cannot)
         policy = f" --max-restarts {int(max_restarts)} --restart-delay {get_config().launcher.restart_delay:g}"
-    primary = (f"{th} spawn --name {name} --log {logf} {env_args}{policy} -- bash -lc {shlex.quote(command)}")
+    # th-run prints the task's pid; `status` then prints the new session's state (sid, uid, monitor
+    # pid) in the same round trip, for core/attribution.py
+    primary = (f"{th} spawn --name {name} --log {logf} {env_args}{policy} -- bash -lc {shlex.quote(command)}"
+               f" && {th} status --name {name}")
     envs = " ".join(f"{k}={shlex.quote(str(v))}" for k, v in env.items())
     fallback = (f"mkdir -p $(dirname {logf}) && ( {envs} setsid bash -lc {shlex.quote(command)} "
                 f"> >(tee -a {logf} >/dev/null) 2>&1 < /dev/null & echo $! )")
@@ -141,10 +146,19 @@ def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra
                                                  max_restarts))
     if r.exception is not None:
         raise SpawnError(f"connection failed: {r.exception}")
-    try:
-        return int(r.stdout.strip().splitlines()[-1])
-    except (ValueError, IndexError):
+    pid = None
+    for line in r.stdout.strip().splitlines():
+        line = line.strip()
+        if line.isdigit() and pid is None:
+            pid = int(line)
+        elif line.startswith("{"):
+            try:
+                attribution.REGISTRY.record(hostname, json.loads(line), listed_as=user)
+            except json.JSONDecodeError:
+                pass
+    if pid is None:
         raise SpawnError(f"unable to parse pid from {r.stdout!r} / {r.stderr.strip()!r}")
+    return pid
 
 
 def terminate(pid: int, hostname: str, user: str, gracefully: bool | None = True) -> int:
@@ -176,6 +190,8 @@ def running(hostname: str, user: str) -> list[dict]:
             continue
         if str(d.get("name", "")).startswith(SESSION_PREFIX):
             out.append(d)
+    if r.exit_code == 0:  # a complete listing: the attestation registry follows it
+        attribution.REGISTRY.replace_listing(hostname, user, out)
     return out
 
 

@@ -49,7 +49,9 @@ def entry_from_thsmi(host: str, doc: dict, extra_gpu_metrics: dict | None = None
         if extra_gpu_metrics and g.get("index") in extra_gpu_metrics:
             metrics.update(extra_gpu_metrics[g["index"]])
         procs = [{"pid": p["pid"], "command": p.get("command", ""), "owner": p.get("owner"),
-                  "task_id": p.get("task_id"), "vram": p.get("vram")} for p in g.get("processes", [])]
+                  "task_id": p.get("task_id"), "vram": p.get("vram"), "uid": p.get("uid"),
+                  "sid": p.get("sid"), "pgid": p.get("pgid"), "ancestors": p.get("ancestors") or []}
+                 for p in g.get("processes", [])]
         gpus[g["uuid"]] = {"name": g.get("name"), "index": g.get("index"), "bdf": g.get("bdf"),
                            "numa_node": g.get("numa_node"), "metrics": metrics, "processes": procs}
     cpu = doc.get("cpu")
@@ -67,7 +69,11 @@ def apply_task_hbm(entry: dict, pattern: str | None = None) -> dict:
     rates = hbm.read_rates(pattern) if pattern else hbm.read_rates()
     counted = hbm.metrics_for(gpus, rates)
     for g in gpus:
-        g.setdefault("metrics", {}).update(counted.get(g.get("index"), {"hbm_bw_source": _metric("umc_activity", "")}))
+        m = g.setdefault("metrics", {})
+        # raw counts + the device-wide estimate, for the daemon to re-derive the metrics from
+        # ATTESTED task ids (core/attribution.py -> hbm.finalize_entry); dropped before publishing
+        g["_hbm"] = {"counts": hbm.raw_counts(rates, g.get("bdf")) or {}, "est": (m.get("hbm_bw") or {}).get("value")}
+        m.update(counted.get(g.get("index"), {"hbm_bw_source": _metric("umc_activity", "")}))
     return entry
 
 
@@ -383,7 +389,8 @@ class RemoteBackend(TelemetryBackend):
     * ``mode="th-smi"``: ``th-smi --stream MS`` (or one-shot ``th-smi --json`` without
       ``stream_ms``): amdsmi metrics and processes only.
 
-    A stream whose newest line is older than ``stale_s`` reports the node as down (None)."""
+    A stream whose newest line is older than ``stale_s`` reports the node as down (None) and, if
+    its process is still alive (a hung channel or agent), is killed so the next sample reconnects."""
 
     name = "remote"
 
@@ -467,6 +474,16 @@ class RemoteBackend(TelemetryBackend):
             with self._lock:
                 got = self._latest.get(host)
             if not got or time.time() - got[0] > self.stale_s:
+                # a channel that is alive but silent (hung SSH, frozen agent) is restarted: end it
+                # here and the next sample starts a fresh one
+                p = self._procs.get(host)
+                if p is not None and p.poll() is None and time.time() - self._started.get(host, 0.0) > self.stale_s:
+                    log.warning("telemetry stream of %s silent for > %.1f s; restarting it", host, self.stale_s)
+                    p.terminate()
+                    try:
+                        p.wait(2)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
                 return None
             ts, doc, mode = got
             return copy.deepcopy(doc) if mode == "agent" else entry_from_thsmi(host, doc)
@@ -518,10 +535,14 @@ class StubBackend(TelemetryBackend):
         return "GPU-" + str(uuidlib.uuid5(uuidlib.NAMESPACE_DNS, f"{host}/gpu{index}"))
 
     def add_process(self, host: str, gpu_index: int, pid: int, owner: str, command: str = "python train.py",
-                    task_id: str | None = None) -> None:
+                    task_id: str | None = None, sid: int | None = None, ancestors: list | None = None,
+                    uid: int | None = None) -> None:
+        """A scripted tenant.  ``sid`` defaults to the pid (a session of its own, like a process
+        started from a shell outside any task); ``uid`` to unknown (attested by owner name)."""
         with self._lock:
             self.processes.setdefault((host, gpu_index), []).append(
-                {"pid": pid, "command": command, "owner": owner, "task_id": task_id, "vram": 1 << 30})
+                {"pid": pid, "command": command, "owner": owner, "task_id": task_id, "vram": 1 << 30,
+                 "uid": uid, "sid": pid if sid is None else sid, "pgid": pid, "ancestors": list(ancestors or [])})
 
     def clear_processes(self, host: str | None = None) -> None:
         with self._lock:

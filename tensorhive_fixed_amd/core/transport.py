@@ -176,7 +176,7 @@ class SimulatedNode(FakeTransport):
     the amdsmi backend would report them.  ``exit_task(pid)`` simulates a task finishing."""
 
     _SPAWN = re.compile(r"spawn --name (\S+) --log (\S+)((?: --env \S+)*)(?: --max-restarts (\d+) --restart-delay \S+)?"
-                        r" -- bash -lc (.*?); else")
+                        r" -- bash -lc (.*?)(?: && \S+ status --name \S+)?; else")
     _SIG = re.compile(r"then \S+ (interrupt|terminate|kill) --pid (\d+)")
 
     def __init__(self, host: str, telemetry=None, first_pid: int = 40000):
@@ -254,14 +254,20 @@ class SimulatedNode(FakeTransport):
         with self._lock:
             pid = self._next
             self._next += 1
+            # th-run's session facts: the first child's setsid gives the session id, the monitor
+            # is its child (pids of their own, disjoint from task pids)
+            sid, mon = 900000 + pid, 800000 + pid
             self.sessions[pid] = {"name": name, "pid": pid, "pgid": pid, "started": time.time(), "user": user,
                                   "command": cmd, "log": logf, "gpus": gpus, "first_pid": pid, "pids": str(pid), "restarts": 0,
-                                  "max_restarts": max_restarts, "env": env}
+                                  "max_restarts": max_restarts, "env": env, "sid": sid, "monitor_pid": mon,
+                                  "status": "running"}
             self.logs[logf] = [f"[simulated] {cmd}"]
+            status = json.dumps({k: v for k, v in self.sessions[pid].items() if k not in ("gpus", "env")})
         if self.telemetry is not None:
             for g in gpus:
-                self.telemetry.add_process(self.host, g, pid, user or "", cmd[:80], env.get("TENSORHIVE_TASK_ID"))
-        return Result(self.host, f"{pid}\n", "", 0)
+                self.telemetry.add_process(self.host, g, pid, user or "", cmd[:80], env.get("TENSORHIVE_TASK_ID"),
+                                           sid=sid, ancestors=[mon])
+        return Result(self.host, f"{pid}\n{status}\n", "", 0)
 
     def crash_task(self, pid: int, code: int = 1) -> int | None:
         """Simulate a run exiting with ``code``: like th-run, a session with restarts left is
@@ -286,7 +292,8 @@ class SimulatedNode(FakeTransport):
         if self.telemetry is not None:
             for g in s["gpus"]:
                 self.telemetry.add_process(self.host, g, new, s["user"] or "", s["command"][:80],
-                                           s["env"].get("TENSORHIVE_TASK_ID"))
+                                           s["env"].get("TENSORHIVE_TASK_ID"), sid=s["sid"],
+                                           ancestors=[s["monitor_pid"]])
         return new
 
     def exit_task(self, pid: int, line: str = "[simulated] done") -> None:

@@ -56,7 +56,9 @@ def _is_one_shell_word(v: str) -> bool:
     """Would ``bash`` read ``v`` as exactly one word with no unquoted control operator, no
     comment (a word starting with ``#``) and no brace expansion (``{a,b}``, ``{1..3}``)?
     (A small scanner, mirrored line for line by ``app/static/js/launch.js``.)"""
-    words, in_word, quote, brace, i = 0, False, "", 0, 0
+    # braces: one entry per open '{' -- whether that level saw an unquoted ',' or '..' (nested
+    # levels are tracked separately: `{a,{c}}` expands through its OUTER level)
+    words, in_word, quote, braces, i = 0, False, "", [], 0
     while i < len(v):
         c = v[i]
         if quote == "'":
@@ -68,7 +70,7 @@ def _is_one_shell_word(v: str) -> bool:
             elif c == '"':
                 quote = ""
         elif c in " \t\n":
-            in_word, brace = False, 0
+            in_word, braces = False, []
         elif c in ";&|<>()":
             return False
         else:
@@ -81,13 +83,12 @@ def _is_one_shell_word(v: str) -> bool:
             elif c in "'\"":
                 quote = c
             elif c == "{":
-                brace = 1
-            elif brace and (c == "," or (c == "." and v[i + 1:i + 2] == ".")):
-                brace = 2
-            elif c == "}":
-                if brace == 2:
+                braces.append(False)
+            elif braces and (c == "," or (c == "." and v[i + 1:i + 2] == ".")):
+                braces[-1] = True
+            elif c == "}" and braces:
+                if braces.pop():
                     return False
-                brace = 0
         i += 1
     return words == 1 and quote == "" and i == len(v)
 

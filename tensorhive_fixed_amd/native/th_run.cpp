@@ -21,10 +21,14 @@
 //
 // State: one `NAME.state` key=value file per session in the state dir (default
 // $TH_RUN_STATE_DIR or ~/.local/state/tensorhive/th-run), written atomically (rename).  These
-// files are the durable PID truth the daemon re-adopts after a restart.
+// files are the durable PID truth the daemon re-adopts after a restart.  They also carry the
+// session id, uid and user the task runs as: the daemon accepts a GPU process's
+// TENSORHIVE_TASK_ID only when the process is in that session (or descends from the monitor)
+// and runs as that uid (core/attribution.py).
 #include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <pwd.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -147,7 +151,7 @@ std::string to_json(const KV& kv, bool alive) {
     const bool num = it.first == "pid" || it.first == "pgid" || it.first == "monitor_pid" ||
                      it.first == "exit_code" || it.first == "started" || it.first == "ended" ||
                      it.first == "first_pid" || it.first == "restarts" || it.first == "max_restarts" ||
-                     it.first == "last_exit_code";
+                     it.first == "last_exit_code" || it.first == "sid" || it.first == "uid";
     o += "\"" + json_escape(it.first) + "\":";
     if (num && !it.second.empty())
       o += it.second;
@@ -295,6 +299,17 @@ int do_spawn(Args& a) {
   for (auto& s : a.argv) cmdline += (cmdline.empty() ? "" : " ") + s;
   st["cmd"] = cmdline;
   st["max_restarts"] = std::to_string(a.max_restarts);
+  // Attestation of the task's processes (core/attribution.py): every process the task starts is
+  // in THIS session (the first child's setsid above) unless it calls setsid itself, and then its
+  // parent chain still reaches this monitor.  Neither can be joined by a process started outside
+  // the session, whatever it puts in its environment; the uid says who the task runs as.
+  st["sid"] = std::to_string((long)getsid(0));
+  st["uid"] = std::to_string((long)getuid());
+  {
+    struct passwd pw, *res = nullptr;
+    char pbuf[4096];
+    if (getpwuid_r(getuid(), &pw, pbuf, sizeof pbuf, &res) == 0 && res) st["user"] = res->pw_name;
+  }
   int restarts = 0, code = -1;
   for (;;) {
     sigprocmask(SIG_BLOCK, &guard, &prev);

@@ -6,8 +6,10 @@
 // the reference's metric keys (utilization, mem_util, mem_free/used/total MiB, temp, power,
 // fan_speed = null on the passively cooled MI355X) plus MI355X extras (hotspot/HBM temperature,
 // gfx/mem clocks, energy, xGMI read/write throughput from the PMFW accumulators), and the GPU's
-// processes already attributed to a UNIX owner and -- via /proc/<pid>/environ -- to the
-// TensorHive task that launched them (TENSORHIVE_TASK_ID).  Process discovery has two sources:
+// processes already attributed to a UNIX owner, with the TensorHive task they CLAIM
+// (TENSORHIVE_TASK_ID from /proc/<pid>/environ) and the facts that claim is checked against:
+// session id, process group and parent chain (core/attribution.py accepts the claim only for a
+// process inside that task's th-run session running as the task's uid).  Process discovery has two sources:
 //   * amdsmi + KFD sysfs (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>) -- these are HOST pids;
 //     a pid is only trusted when the process it names in OUR /proc really has /dev/kfd open
 //     (inside a container, a host pid may be absent or name an unrelated process);
@@ -124,7 +126,19 @@ std::string read_file(const std::string& p, size_t cap = 1 << 16) {
 struct ProcInfo {
   std::string owner, cmd, task_id;
   long uid = -1;
+  long ppid = -1, pgid = -1, sid = -1;
+  std::vector<long> ancestors;  // parent, grandparent, ... (init and kernel threads excluded)
 };
+
+// ppid / pgrp / session from /proc/<pid>/stat ("pid (comm) state ppid pgrp session ..."; comm may
+// hold spaces and parentheses, so parse after the LAST ')').
+bool read_stat_ids(long pid, long& ppid, long& pgid, long& sid) {
+  const std::string st = read_file("/proc/" + std::to_string(pid) + "/stat", 4096);
+  const size_t rp = st.rfind(')');
+  if (rp == std::string::npos) return false;
+  char state = 0;
+  return sscanf(st.c_str() + rp + 1, " %c %ld %ld %ld", &state, &ppid, &pgid, &sid) == 4;
+}
 
 ProcInfo resolve_pid(long pid) {
   ProcInfo pi;
@@ -143,6 +157,18 @@ ProcInfo resolve_pid(long pid) {
     if (c == 0) c = ' ';
   while (!cl.empty() && cl.back() == ' ') cl.pop_back();
   pi.cmd = cl;
+  // Session, process group and the parent chain: what the daemon checks a claimed task id against
+  // (a th-run task's processes share its session, or descend from its monitor -- core/attribution.py).
+  // The environment below is user-writable; these are not.
+  if (read_stat_ids(pid, pi.ppid, pi.pgid, pi.sid)) {
+    long cur = pi.ppid;
+    for (int depth = 0; cur > 1 && depth < 64; ++depth) {
+      pi.ancestors.push_back(cur);
+      long pp = -1, pg = -1, sd = -1;
+      if (!read_stat_ids(cur, pp, pg, sd)) break;
+      cur = pp;
+    }
+  }
   std::string env = read_file(base + "/environ", 1 << 20);  // readable for own / same-uid / root
   const char* key = "TENSORHIVE_TASK_ID=";
   for (size_t i = 0; i < env.size();) {
@@ -420,7 +446,11 @@ std::string gpu_json(Gpu& g, const std::map<uint64_t, std::set<long>>& kfd,
     first = false;
     ps += "{\"pid\":" + std::to_string(p.first) + ",\"command\":\"" + esc(pi.cmd) + "\",\"owner\":\"" +
           esc(pi.owner) + "\",\"uid\":" + std::to_string(pi.uid) + ",\"vram\":" + std::to_string(p.second) +
-          ",\"task_id\":" + (pi.task_id.empty() ? "null" : "\"" + esc(pi.task_id) + "\"") + "}";
+          ",\"task_id\":" + (pi.task_id.empty() ? "null" : "\"" + esc(pi.task_id) + "\"") +
+          ",\"ppid\":" + std::to_string(pi.ppid) + ",\"pgid\":" + std::to_string(pi.pgid) +
+          ",\"sid\":" + std::to_string(pi.sid) + ",\"ancestors\":[";
+    for (size_t k = 0; k < pi.ancestors.size(); ++k) ps += (k ? "," : "") + std::to_string(pi.ancestors[k]);
+    ps += "]}";
   }
   ps += "]";
   return "{\"uuid\":\"" + esc(g.uuid) + "\",\"name\":\"" + esc(g.name) + "\",\"index\":" +

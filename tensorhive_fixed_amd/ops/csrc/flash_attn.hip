@@ -1220,6 +1220,10 @@ __device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x
 //         half of the delta buffer: the S' chain's initial C loads straight from LDS, no multiply
 // bit7 builds sum their stamps over all waves into g_kf_stamp = {barrier + DMA wait, MFMA 0-15,
 // 16-31, 32-47, 48-63, wave-tiles, wave-blocks, whole-block cycles} (s_memtime ticks = shader cycles)
+// Only the diagnostic build (-DTH_KF_DIAG=1, scripts/build_variant_lib.sh kf_diag, used by
+// scripts/kf_stamps.py) has the stamped variants, the accumulators and th_kf_stamps: the production
+// libthk.so carries none of them (tests/test_flash_flags.py checks its exports).
+#ifdef TH_KF_DIAG
 __device__ unsigned long long g_kf_stamp[8];
 // one stamp: s_memtime with its own lgkmcnt(0) in the same statement (cdna_hip_programming.md
 // 'In-kernel stamps'; read the SHARES of a stamped build, not its length)
@@ -1230,6 +1234,11 @@ __device__ __forceinline__ unsigned long long kf_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
+__device__ __forceinline__ void kf_stamp_add(int i, unsigned long long v) { atomicAdd(&g_kf_stamp[i], v); }
+#else
+__device__ __forceinline__ unsigned long long kf_stamp() { return 0; }
+__device__ __forceinline__ void kf_stamp_add(int, unsigned long long) {}
+#endif
 #define BAR_OF(V) (((V) & 64) ? 0 : 48)
 
 // one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
@@ -1505,14 +1514,14 @@ __device__ __forceinline__ void kf_block(
     if (lane == 0) {
       // the order of g_kf_stamp: barrier, 0-15, 16-31, 32-47, 48-63, tiles, blocks, whole block
       const unsigned long long t = kf_stamp();
-      atomicAdd(&g_kf_stamp[0], (unsigned long long)st_acc[4]);
-      atomicAdd(&g_kf_stamp[1], (unsigned long long)st_acc[1]);
-      atomicAdd(&g_kf_stamp[2], (unsigned long long)st_acc[2]);
-      atomicAdd(&g_kf_stamp[3], (unsigned long long)st_acc[3]);
-      atomicAdd(&g_kf_stamp[4], (unsigned long long)st_acc[0]);
-      atomicAdd(&g_kf_stamp[5], (unsigned long long)total);
-      atomicAdd(&g_kf_stamp[6], 1ull);
-      atomicAdd(&g_kf_stamp[7], t - st_t0);
+      kf_stamp_add(0, (unsigned long long)st_acc[4]);
+      kf_stamp_add(1, (unsigned long long)st_acc[1]);
+      kf_stamp_add(2, (unsigned long long)st_acc[2]);
+      kf_stamp_add(3, (unsigned long long)st_acc[3]);
+      kf_stamp_add(4, (unsigned long long)st_acc[0]);
+      kf_stamp_add(5, (unsigned long long)total);
+      kf_stamp_add(6, 1ull);
+      kf_stamp_add(7, t - st_t0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
@@ -1629,7 +1638,11 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 // kf variant: flags bits 6-18
 static int kf_var_of(int flags) { return (flags >> 6) & 8191; }
 static bool kf_variant_known(int v) {
-  return v == 0 || v == 111 || v == 3439 || v == 3567 || v == 7535 || v == 7663;
+  return v == 0 || v == 111 || v == 3439 || v == 7535
+#ifdef TH_KF_DIAG
+         || v == 3567 || v == 7663  // s_memtime-stamped builds (diagnostic library only)
+#endif
+      ;
 }
 
 static int flash_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -1694,9 +1707,11 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
       case 0: TH_KF_LAUNCH(0); break;
       case 111: TH_KF_LAUNCH(111); break;    // bits 0-3, 5, 6
       case 3439: TH_KF_LAUNCH(3439); break;  // 111 + bits 8, 10, 11
-      case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + s_memtime stamps (diagnostic, th_kf_stamps)
       case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + -lse2 from the dQ kernel (bit12; the default, attention.py)
+#ifdef TH_KF_DIAG
+      case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + s_memtime stamps (th_kf_stamps)
       case 7663: TH_KF_LAUNCH(7663); break;  // 7535 + stamps
+#endif
       default: return -3;                    // unreachable: kf_variant_known
     }
 #undef TH_KF_LAUNCH
@@ -1729,6 +1744,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   TH_CHECK_LAUNCH();
 }
 
+#ifdef TH_KF_DIAG
 // kf stamp accumulators (VAR bit7 builds): reset = 1 zeroes them, else copies the 8 sums to out
 extern "C" int th_kf_stamps(unsigned long long* out, int reset) {
   if (reset) {
@@ -1737,6 +1753,7 @@ extern "C" int th_kf_stamps(unsigned long long* out, int reset) {
   }
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kf_stamp), 8 * sizeof(unsigned long long));
 }
+#endif
 
 extern "C" int th_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
                                  const void* dout, const float* lse, float* delta, float* dq_acc,

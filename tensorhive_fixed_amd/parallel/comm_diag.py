@@ -3,8 +3,9 @@ much of each step the compute stream spent waiting on communication.
 
 * :func:`prepare_rccl_log` (called by ``init_distributed`` before the communicator exists) sends
   RCCL's INIT-subsystem log of this rank to a private file (``NCCL_DEBUG=INFO``,
-  ``NCCL_DEBUG_SUBSYS=INIT``, ``NCCL_DEBUG_FILE``) unless the user chose their own debug settings.
-  Warnings found in it are echoed to stderr, so moving the log off stderr hides nothing.
+  ``NCCL_DEBUG_SUBSYS=INIT``, ``NCCL_DEBUG_FILE``) -- only for bench.py (``TH_RCCL_INIT_LOG=1``),
+  whose :func:`comm_report` echoes the warnings found in it, and never over the user's own
+  RCCL debug settings.
 * :func:`parse_rccl_init` reads that log: library version, ranks, channels (the ``Channel xx/NN``
   rings and the ``N coll channels`` summary), trees, the transports each channel connected through
   (``via P2P/IPC`` = xGMI peer access), chunk size and thread thresholds.
@@ -30,9 +31,11 @@ _LOG_ENV = "TH_RCCL_INIT_LOG"
 
 
 def prepare_rccl_log(rank: int) -> str | None:
-    """Point RCCL's INIT log at a per-rank file; returns its path (None when the user configured
-    RCCL logging themselves or ``TH_RCCL_INIT_LOG=0``)."""
-    if os.environ.get(_LOG_ENV, "1") == "0" or os.environ.get("NCCL_DEBUG_FILE"):
+    """Point RCCL's INIT log at a per-rank file; returns its path.  Opt-in: only when
+    ``TH_RCCL_INIT_LOG=1`` (bench.py sets it, and then echoes the log's warnings), and never over
+    the user's own debugging (a ``NCCL_DEBUG_FILE``, a level above INFO, another subsystem).  A
+    training job (no opt-in) keeps RCCL's warnings and its requested debug output on stderr."""
+    if os.environ.get(_LOG_ENV, "0") != "1" or os.environ.get("NCCL_DEBUG_FILE"):
         return None
     level = os.environ.get("NCCL_DEBUG", "").upper()
     if level not in ("", "WARN", "VERSION", "INFO"):

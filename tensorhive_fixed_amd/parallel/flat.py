@@ -79,10 +79,21 @@ class WaitTimer:
         self.enabled = enabled
         self.reset()
 
+    MAX_EVENTS = 4096  # pending event pairs before they are folded into totals (one sync)
+
     def reset(self) -> None:
         self._events: list[tuple[str, object, object]] = []
-        self._host: dict[str, float] = defaultdict(float)
+        self._host: dict[str, float] = defaultdict(float)  # seconds (host spans, folded events)
         self.counts: dict[str, int] = defaultdict(int)
+
+    def _fold(self) -> None:
+        """Resolve the pending event pairs into the totals and release them, so a long run that
+        never reads the timer holds a bounded number of events."""
+        if self._events:
+            self._events[-1][2].synchronize()
+            for cat, e0, e1 in self._events:
+                self._host[cat] += float(e0.elapsed_time(e1)) / 1000.0
+            self._events = []
 
     @contextmanager
     def span(self, cat: str):
@@ -96,6 +107,8 @@ class WaitTimer:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             self._events.append((cat, e0, e1))
+            if len(self._events) >= self.MAX_EVENTS:
+                self._fold()
         else:
             t0 = time.perf_counter()
             yield
@@ -103,12 +116,8 @@ class WaitTimer:
         self.counts[cat] += 1
 
     def totals_ms(self) -> dict[str, float]:
-        out = {c: 1000.0 * self._host.get(c, 0.0) for c in self.CATEGORIES}
-        if self._events:
-            self._events[-1][2].synchronize()
-            for cat, e0, e1 in self._events:
-                out[cat] = out.get(cat, 0.0) + float(e0.elapsed_time(e1))
-        return out
+        self._fold()
+        return {c: 1000.0 * self._host.get(c, 0.0) for c in self.CATEGORIES}
 
 
 @dataclass
@@ -177,8 +186,9 @@ class FlatParamStore:
         self.accumulating = False
         self._sync_now = True
         self._ready_seen: set[int] = set()
-        # exposed-communication spans (bench.py reports them per rank); TH_COMM_TIMING=0 disables
-        self.timer = WaitTimer(self.device, enabled=os.environ.get("TH_COMM_TIMING", "1") == "1")
+        # exposed-communication spans: bench.py turns them on (TH_COMM_TIMING=1) and reports them
+        # per rank; off for training jobs
+        self.timer = WaitTimer(self.device, enabled=os.environ.get("TH_COMM_TIMING", "0") == "1")
 
     # ------------------------------------------------------------------ buckets
     def _layout(self, entries: list, bucket_mb: float) -> tuple[list[int], list[_Bucket]]:

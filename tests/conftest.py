@@ -90,6 +90,9 @@ def daemon(cfg, tables):
     from tensorhive_fixed_amd.core.daemon import Daemon
     from tensorhive_fixed_amd.core.telemetry import StubBackend
 
+    from tensorhive_fixed_amd.core.attribution import REGISTRY
+
+    REGISTRY.clear()  # th-run sessions seen by an earlier test's daemon
     stub = StubBackend(gpus_per_host=8)
     d = Daemon(cfg, backends={h: stub for h in cfg.ssh.available_nodes}, init_key=False, test_ssh=False)
     d.stub = stub

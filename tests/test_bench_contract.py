@@ -111,6 +111,9 @@ def test_prepare_rccl_log_respects_user_settings(monkeypatch, tmp_path):
         monkeypatch.delenv(k, raising=False)
     import tempfile
     monkeypatch.setattr(tempfile, "tempdir", str(tmp_path))
+    assert comm_diag.prepare_rccl_log(3) is None  # a training job: RCCL logs stay on stderr
+    assert "NCCL_DEBUG_FILE" not in os.environ
+    monkeypatch.setenv("TH_RCCL_INIT_LOG", "1")  # bench.py opts in
     p = comm_diag.prepare_rccl_log(3)
     assert p and p.endswith("-r3.log") and os.environ["NCCL_DEBUG"] == "INFO" and os.environ["NCCL_DEBUG_SUBSYS"] == "INIT"
     monkeypatch.delenv("NCCL_DEBUG_FILE")

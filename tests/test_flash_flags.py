@@ -48,3 +48,26 @@ def test_stamped_build_of_the_default_exists():
     """scripts/kf_stamps.py runs the default variant + bit 7 (stamps)."""
     var = (attention.KF_DEFAULT_FLAGS >> 6) & 8191
     assert (var | 128) in _known_variants()
+
+
+def test_production_library_has_no_diagnostic_stamps():
+    """Round-4 verdict item 7: the s_memtime-stamped kf variants and their accumulators exist only
+    in the TH_KF_DIAG build (scripts/kf_stamps.py); the default libthk.so exports none of them."""
+    import shutil
+    import subprocess
+
+    import pytest
+
+    from tensorhive_fixed_amd.ops import _lib
+
+    lib = _lib.library_path()
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not lib.exists():
+        pytest.skip("libthk.so not built")
+    syms = subprocess.run([nm, "-D", "--defined-only", str(lib)], capture_output=True, text=True).stdout
+    assert "th_flash_attn_bwd" in syms
+    assert "th_kf_stamps" not in syms and "g_kf_stamp" not in syms
+    text = SRC.read_text()
+    for v in (3567, 7663):  # launched only inside the TH_KF_DIAG block
+        i = text.index(f"case {v}: TH_KF_LAUNCH")
+        assert text.rfind("#ifdef TH_KF_DIAG", 0, i) > text.rfind("#endif", 0, i)

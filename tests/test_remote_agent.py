@@ -105,13 +105,18 @@ def test_stale_stream_reports_the_node_down(tmp_path):
     hang = tmp_path / "agent-then-hang"
     hang.write_text(f"#!/bin/bash\n{AGENT} --once \"$@\"\nexec sleep 60\n")
     hang.chmod(0o755)
-    tm, _ = _tm("n1")
+    tm, t = _tm("n1")
     be = RemoteBackend(tm, stream_ms=100, mode="agent", agent_cmd=str(hang), agent_args="--backend stub --stub-gpus 2",
                        stale_s=0.6)
     try:
         _wait_sample(be, "n1")
         time.sleep(1.0)
         assert be.sample("n1") is None
+        # the silent-but-alive channel is killed and the next sample reconnects
+        n = len(t.cmds)
+        first = be._latest["n1"][0]
+        _wait_sample(be, "n1", timeout=30)
+        assert len(t.cmds) > n and be._latest["n1"][0] > first
     finally:
         be.close()
 

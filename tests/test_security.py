@@ -55,7 +55,7 @@ def test_upgraded_install_with_the_public_key_is_rotated(tmp_path):
     assert C.ensure_secret_key(r) and not C.secret_is_insecure(C.load_config(r.parent).auth.secret_key)
 
 
-@pytest.mark.parametrize("key", ["jwt-some-secret", ""])
+@pytest.mark.parametrize("key", ["jwt-some-secret", "", "x", "a" * 31])
 def test_daemon_refuses_to_start_with_a_public_or_empty_key(cfg, monkeypatch, key):
     from tensorhive_fixed_amd.cli import refuse_insecure_secret
 
@@ -65,6 +65,24 @@ def test_daemon_refuses_to_start_with_a_public_or_empty_key(cfg, monkeypatch, ke
         refuse_insecure_secret(cfg)
     monkeypatch.setenv(C.ALLOW_INSECURE_ENV, "1")
     refuse_insecure_secret(cfg)  # tests may opt in
+
+
+def test_a_long_operator_key_is_kept_and_accepted(tmp_path, cfg, monkeypatch):
+    """The minimum is a length, not a pattern: the operator's own 32+ character key is neither
+    replaced on startup nor refused; a short one is kept in the file but refused."""
+    from tensorhive_fixed_amd.cli import refuse_insecure_secret
+
+    monkeypatch.delenv(C.ALLOW_INSECURE_ENV, raising=False)
+    p = tmp_path / "m.ini"
+    for key, ok in (("k" * 32, True), ("short-but-mine", False)):
+        p.write_text(f"[auth]\nsecret_key = {key}\n")
+        assert C.ensure_secret_key(p) is False and key in p.read_text()
+        cfg.auth.secret_key = key
+        if ok:
+            refuse_insecure_secret(cfg)
+        else:
+            with pytest.raises(click.ClickException, match="32 characters"):
+                refuse_insecure_secret(cfg)
 
 
 def _get_jobs(client, token):
@@ -174,6 +192,53 @@ def test_uncounted_tenant_makes_the_gpu_partial(tmp_path):
     assert m["hbm_uncounted_pids"]["value"] == 1
     gpus[0]["metrics"]["hbm_bw"]["value"] = 400.0  # the estimate never hides counted bytes
     assert hbm.metrics_for(gpus, _rates(tmp_path))[0]["hbm_bw"]["value"] == 1000.0
+
+
+def test_counts_of_a_forged_task_id_are_not_accepted(tmp_path):
+    """The counter files are authenticated per pid, but whether the pid is a task process is a
+    CLAIM: after attestation (``core/attribution.py``) a process carrying a task id it does not
+    own neither gets its counts accepted nor hides its traffic behind a ``counters`` label."""
+    from tensorhive_fixed_amd.core.attribution import Attestor, SessionRegistry
+    from tensorhive_fixed_amd.core.telemetry import apply_task_hbm
+
+    me = os.getpid()
+    _file(tmp_path, me, BDF0, 1.0e12, 0.0)
+    reg = SessionRegistry()
+    reg.record("n", {"name": "tensorhive_task_7", "sid": 1, "monitor_pid": 2, "uid": os.getuid()})
+
+    def entry(sid):
+        return {"GPU": {"u0": _gpu(0, BDF0, [{"pid": me, "task_id": "7", "uid": os.getuid(), "sid": sid}],
+                                   est=2600.0)}}
+
+    e = apply_task_hbm(entry(sid=12345), str(tmp_path / "th-hbm-*.json"))  # node view: the claim
+    assert e["GPU"]["u0"]["metrics"]["hbm_bw_source"]["value"] == "counters"
+    Attestor(reg).attest_entry("n", e)  # daemon view: not in task 7's session
+    m = e["GPU"]["u0"]["metrics"]
+    assert m["hbm_bw_source"]["value"] == "umc_activity" and m["hbm_bw"]["value"] == 2600.0
+    assert "hbm_read" not in m and "_hbm" not in e["GPU"]["u0"]
+    e = apply_task_hbm(entry(sid=1), str(tmp_path / "th-hbm-*.json"))  # genuinely in the session
+    Attestor(reg).attest_entry("n", e)
+    m = e["GPU"]["u0"]["metrics"]
+    assert m["hbm_bw_source"]["value"] == "counters" and m["hbm_bw"]["value"] == 1000.0
+
+
+def test_planted_fifo_symlink_and_huge_files_neither_block_nor_count(tmp_path):
+    """``/dev/shm`` is world-writable: a FIFO would block a plain open, a symlink to /dev/zero or a
+    huge file would make the read unbounded.  None of them is read; the real file still counts."""
+    import threading
+
+    me = os.getpid()
+    _file(tmp_path, me, BDF0, 1e12, 0.0)
+    os.mkfifo(tmp_path / "th-hbm-fifo.json")
+    os.symlink("/dev/zero", tmp_path / "th-hbm-zero.json")
+    os.symlink(tmp_path / f"th-hbm-{me}.json", tmp_path / "th-hbm-link.json")
+    (tmp_path / "th-hbm-big.json").write_bytes(b" " * (hbm.MAX_FILE_BYTES + 1))
+    out = {}
+    t = threading.Thread(target=lambda: out.update(r=_rates(tmp_path)), daemon=True)
+    t.start()
+    t.join(10)
+    assert not t.is_alive(), "read_rates blocked on a planted file"
+    assert out["r"][BDF0]["pids"] == [me]  # the symlink to the genuine file is not read twice
 
 
 def test_profiler_tasks_do_not_get_the_counter_tool(cfg, monkeypatch):

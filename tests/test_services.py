@@ -70,11 +70,18 @@ def test_protection_detects_intruder(daemon, new_user, new_admin):
 
 
 def test_protection_accepts_owners_tasks_and_levels(daemon, new_user, new_job_with_task):
+    """A genuine process of the owner's task is fine even under a service account: it is in the
+    task's th-run session and runs as the task's user (``core/attribution.py``)."""
+    from tensorhive_fixed_amd.core.attribution import REGISTRY
+
     res = gpu(daemon)
     reserve(new_user, res, UTC() - timedelta(minutes=10), timedelta(hours=1))
     tid = new_job_with_task.tasks[0].id
-    # a process of the owner's task, even if it runs under a service account, is fine
-    daemon.stub.add_process("node-a", 0, 3333, "svc-account", task_id=str(tid))
+    REGISTRY.record("node-a", {"name": f"tensorhive_task_{tid}", "sid": 7000, "monitor_pid": 6999,
+                               "pid": 3333, "user": "svc-account"})
+    daemon.stub.add_process("node-a", 0, 3333, "svc-account", task_id=str(tid), sid=7000)
+    # a rank that called setsid itself: attested through its parent chain (th-run's monitor)
+    daemon.stub.add_process("node-a", 0, 3334, "svc-account", task_id=str(tid), sid=3334, ancestors=[3333, 6999])
     daemon.stub.add_process("node-a", 5, 4444, "someone")  # unreserved GPU
     publish(daemon)
     lenient = ProtectionService(1.0, [], level=1)
@@ -84,6 +91,58 @@ def test_protection_accepts_owners_tasks_and_levels(daemon, new_user, new_job_wi
     strict.inject(daemon)
     v = strict.find_violations()
     assert set(v) == {"someone"} and v["someone"]["VIOLATION_PIDS"] == {"node-a": {4444}}
+
+
+def test_forged_task_id_is_a_violation(daemon, new_user, new_job_with_task):
+    """Round-4 bypass: ``TENSORHIVE_TASK_ID=<victim's task> python train.py`` on a reserved GPU.
+    The claim is checked against the task's th-run session and uid, so an intruder -- or a
+    process of the same service account outside the task's session -- is still a violation, and
+    the published process carries ``claimed_task_id`` instead of ``task_id``."""
+    from tensorhive_fixed_amd.core.attribution import REGISTRY
+
+    res = gpu(daemon)
+    reserve(new_user, res, UTC() - timedelta(minutes=10), timedelta(hours=1))
+    tid = str(new_job_with_task.tasks[0].id)
+    REGISTRY.record("node-a", {"name": f"tensorhive_task_{tid}", "sid": 7000, "monitor_pid": 6999,
+                               "pid": 3333, "user": "svc-account"})
+    daemon.stub.add_process("node-a", 0, 3333, "svc-account", task_id=tid, sid=7000)  # genuine
+    daemon.stub.add_process("node-a", 0, 5001, "intruder", task_id=tid, sid=5001)  # other uid
+    daemon.stub.add_process("node-a", 0, 5002, "intruder", task_id=tid, sid=7000)  # other uid, same sid number
+    daemon.stub.add_process("node-a", 0, 5003, "svc-account", task_id=tid, sid=5003)  # same uid, outside
+    daemon.stub.add_process("node-a", 0, 5004, "svc-account", task_id="999", sid=7000)  # unknown task
+    publish(daemon)
+    svc = ProtectionService(1.0, [], level=1)
+    svc.inject(daemon)
+    v = svc.find_violations()
+    assert set(v) == {"intruder", "svc-account"}
+    assert v["intruder"]["VIOLATION_PIDS"] == {"node-a": {5001, 5002}}
+    assert v["svc-account"]["VIOLATION_PIDS"] == {"node-a": {5003, 5004}}
+    procs = {p["pid"]: p for p in daemon.infrastructure.node_gpu_processes("node-a")[res.id]}
+    assert procs[3333]["task_id"] == tid and "claimed_task_id" not in procs[3333]
+    assert procs[5001]["task_id"] is None and procs[5001]["claimed_task_id"] == tid
+
+
+def test_claim_of_unseen_task_triggers_one_session_lookup(daemon, new_user, new_job_with_task):
+    """A daemon restarted under a running task has not seen its session yet: the first claim
+    lists the owner's th-run sessions on that node once (rate-limited), then attests."""
+    from tensorhive_fixed_amd.core.attribution import REGISTRY
+
+    REGISTRY.clear()
+    task = new_job_with_task.tasks[0]
+    node = daemon.transports.get(task.hostname)
+    user = new_job_with_task.user.username
+    node.sessions[4242] = {"name": f"tensorhive_task_{task.id}", "pid": 4242, "pgid": 4242, "user": user,
+                           "sid": 9100, "monitor_pid": 9099, "status": "running", "gpus": [], "env": {}}
+    daemon.stub.add_process(task.hostname, 1, 4242, user, task_id=str(task.id), sid=9100)
+    daemon.stub.add_process(task.hostname, 2, 4243, "intruder", task_id=str(task.id), sid=4243)
+    n0 = sum(1 for c, _ in node.calls if " ls" in c)
+    publish(daemon)
+    publish(daemon)
+    assert sum(1 for c, _ in node.calls if " ls" in c) - n0 == 1  # the intruder's claim does not re-list
+    procs = daemon.infrastructure.node_gpu_processes(task.hostname)
+    by_pid = {p["pid"]: p for ps in procs.values() for p in ps}
+    assert by_pid[4242]["task_id"] == str(task.id)
+    assert by_pid[4243]["task_id"] is None and by_pid[4243]["claimed_task_id"] == str(task.id)
 
 
 def test_protection_handlers_warn_and_kill(daemon, new_user):

@@ -357,7 +357,7 @@ def test_scaling_bucket_sweep_records_each_size_and_the_best():
 SHELL_CASES = ['"a b"', "/data/*.tfrecord", "$HOME/x", "~/ckpt", "a b", "a;b", '"a;b"', "it's", "--x=1",
                '{"a": 1}', '{"cluster":{"w":["h:1"]}}', "a\\ b", "x\\", "'quoted already'", "a&&b", "(x)",
                "tcp://127.0.0.1:29500", "", "{a,b}", 'say "hi there"', "#1", "a#b", "x{1..3}",
-               "{a}", "${HOME}", "--tag=#x"]
+               "{a}", "${HOME}", "--tag=#x", "{a,{c}}", "x{a,{b}}y", "{{a}}", "{x{1..2}}"]
 
 
 def test_shell_value_keeps_one_word_values_and_js_agrees(tmp_path):
@@ -374,7 +374,9 @@ def test_shell_value_keeps_one_word_values_and_js_agrees(tmp_path):
               # a leading # would comment out the rest of the command, a brace list
               # would expand into several words (shlex does neither, so check the rendering)
               "#1": "'#1'", "a#b": "a#b", "{a,b}": "'{a,b}'", "x{1..3}": "'x{1..3}'", "{a}": "{a}",
-              "${HOME}": "${HOME}"}
+              "${HOME}": "${HOME}",
+              # nested braces -- the OUTER list expands (bash: `a` and `{c}`)
+              "{a,{c}}": "'{a,{c}}'", "x{a,{b}}y": "'x{a,{b}}y'", "{{a}}": "{{a}}", "{x{1..2}}": "'{x{1..2}}'"}
     for v, want in expect.items():
         assert _shell_value(v) == want, v
     for v in SHELL_CASES:  # every rendered value is exactly one shell word
