@@ -15,6 +15,9 @@ with exactly the code the daemon uses for its own node (:class:`AmdSmiBackend`):
   started with ``[launcher] hbm_tool``), authenticated and merged per GPU (``core/hbm.py``);
 * optionally the device-wide counter sampler (``th-counters``).
 
+With ``--events SOCK`` the agent also listens for th-run's task-exit datagrams (``core/events.py``):
+on one it samples the node at once and sends ``{"v": 1, ..., "event": {...}}`` after that entry.
+
 Every line is ``{"v": 1, "ts": <unix s>, "host": <node>, "entry": <infrastructure entry>}``; the
 entry is the same per-host document the local backend publishes, so the API, protection,
 allocation and usage logging see remote GPUs exactly like local ones.  The agent exits (and stops
@@ -79,6 +82,9 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--stub-gpus", type=int, default=8)
     ap.add_argument("--stub-process", action="append", metavar="GPU:PID:OWNER[:TASK]")
     ap.add_argument("--hbm-glob", default=None, help="counter files to merge (default /dev/shm/th-hbm-*.json)")
+    ap.add_argument("--events", default=None, metavar="SOCK",
+                    help="unix datagram socket th-run notifies on task exit (core/events.py): the agent "
+                         "samples the node at once and forwards the event")
     args = ap.parse_args(argv)
 
     stop = {"flag": False}
@@ -90,28 +96,64 @@ def main(argv: list[str] | None = None) -> int:
         signal.signal(sig, _stop)
     backend = build_backend(args)
     period = max(0.02, args.stream / 1000.0) if args.stream > 0 else 0.0
+    ev_sock = None
+    if args.events and period > 0:
+        from .core.events import open_event_socket
+
+        try:
+            ev_sock, _path, _tmp = open_event_socket(args.events)
+        except OSError as e:  # another agent's socket, a squatted path: exits are found by polling
+            print(json.dumps({"v": 1, "warning": f"task events unavailable: {e}"[:300]}), flush=True)
     rc = 0
+
+    def emit(doc) -> bool:
+        try:
+            sys.stdout.write(json.dumps(doc, separators=(",", ":")) + "\n")
+            sys.stdout.flush()
+            return True
+        except BrokenPipeError:  # the SSH channel is gone: stop the probe with us
+            return False
+
     try:
+        events: list[dict] = []
         while not stop["flag"]:
             t0 = time.monotonic()
             entry = sample(backend, args)
-            line = json.dumps({"v": 1, "ts": round(time.time(), 3), "host": args.host, "entry": entry},
-                              separators=(",", ":"))
-            try:
-                sys.stdout.write(line + "\n")
-                sys.stdout.flush()
-            except BrokenPipeError:  # the SSH channel is gone: stop the probe with us
+            if not emit({"v": 1, "ts": round(time.time(), 3), "host": args.host, "entry": entry}):
                 break
+            # task exits that arrived: forwarded AFTER a sample taken once they had happened
+            if events and not all(emit({"v": 1, "ts": round(time.time(), 3), "host": args.host, "event": ev})
+                                  for ev in events):
+                break
+            events = []
             if args.once or period == 0.0:
                 break
             left = period - (time.monotonic() - t0)
             while left > 0 and not stop["flag"]:
-                time.sleep(min(left, 0.05))
+                if ev_sock is not None:
+                    import select
+
+                    from .core.events import parse_event
+
+                    r, _, _ = select.select([ev_sock], [], [], min(left, 0.05))
+                    if r:
+                        ev = parse_event(ev_sock.recv(65536))
+                        if ev is not None:
+                            events.append(ev)
+                            break  # sample now
+                else:
+                    time.sleep(min(left, 0.05))
                 left = period - (time.monotonic() - t0)
     except Exception as e:  # noqa: BLE001 -- report and exit non-zero; the daemon restarts us
         print(json.dumps({"v": 1, "error": f"{type(e).__name__}: {e}"[:300]}), flush=True)
         rc = 1
     finally:
+        if ev_sock is not None:
+            try:
+                ev_sock.close()
+                os.unlink(args.events)
+            except OSError:
+                pass
         try:
             backend.close()
         except Exception:  # noqa: BLE001

@@ -628,6 +628,14 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
             prev = [e for e in ends if e <= starts[j]]
             if prev and enq[j] < prev[-1] and starts[j] - prev[-1] < 60:  # waited for a device a job freed
                 handoff.append((starts[j] - prev[-1]) * 1e3)
+        # the daemon's part of it: th-run's exit time (its task-exit event, core/events.py) -> the
+        # next waiting job's launch; the rest of `handoff` is the job's own teardown after "done"
+        exits = sorted(ev.get("ended_ms", ts * 1e3) / 1e3 for ts, _h, ev in daemon.task_events)
+        handoff_exit = []
+        for j in sorted(starts, key=starts.get):
+            prev = [e for e in exits if e <= starts[j]]
+            if prev and enq[j] < prev[-1] and starts[j] - prev[-1] < 60:
+                handoff_exit.append((starts[j] - prev[-1]) * 1e3)
         statuses = {}
         for j in enq:
             st = Job.get(j).status.name
@@ -671,6 +679,9 @@ def multitenant_node(jobs_per_user: int = 2, seed: int = 0, duration_s: tuple[fl
                 "job_startup_p50_ms": round(_pct(startup, 0.5), 1) if startup else None,
                 "handoff_p50_ms": round(_pct(handoff, 0.5), 1) if handoff else None,
                 "handoff_max_ms": round(max(handoff), 1) if handoff else None,
+                "handoff_from_exit_p50_ms": round(_pct(handoff_exit, 0.5), 1) if handoff_exit else None,
+                "handoff_from_exit_max_ms": round(max(handoff_exit), 1) if handoff_exit else None,
+                "task_exit_events": len(daemon.task_events),
                 "violation": None if hit is None else {
                     "intruder": hit["INTRUDER_USERNAME"], "reserved_by": [r["OWNER_USERNAME"] for r in hit["RESERVATIONS"]],
                     "detect_ms": detect_ms},

@@ -329,6 +329,10 @@ class LauncherConfig:
     # node-local path of libthhbm.so on REMOTE nodes (empty = remote tasks are not counted); the
     # daemon's own node always uses this install's copy
     hbm_tool: str = ""
+    # task exits as events (core/events.py): th-run notifies the daemon (its own node) or the node
+    # agent (remote nodes, on this socket path of the node) when a task has ended
+    task_events: bool = True
+    node_events_socket: str = "/tmp/tensorhive-agent-events.sock"
 
 
 @dataclass
@@ -501,6 +505,8 @@ def load_config(directory: Path | str | None = None) -> Config:
             rccl_algo=main.str("launcher", "rccl_algo", ""),
             rccl_proto=main.str("launcher", "rccl_proto", ""),
             hbm_tool=main.str("launcher", "hbm_tool", ""),
+            task_events=main.bool("launcher", "task_events", True),
+            node_events_socket=main.str("launcher", "node_events_socket", "/tmp/tensorhive-agent-events.sock"),
         ),
     )
 

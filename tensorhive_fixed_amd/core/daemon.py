@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import logging
 import threading
+import time
 
 from ..config import Config, get_config
 from ..utils.exceptions import ConfigurationException
@@ -63,7 +64,9 @@ class Daemon:
                                  stream_ms=int(1000 * self.cfg.monitoring.update_interval),
                                  counters=am.counters_enabled, counters_period_ms=am.counters_period_ms,
                                  task_hbm=am.task_hbm_counters, remote_mode=am.remote_mode,
-                                 remote_agent=am.remote_agent)
+                                 remote_agent=am.remote_agent,
+                                 events_socket=(self.cfg.launcher.node_events_socket
+                                                if self.cfg.launcher.task_events else None))
                 # one StubBackend / AmdSmiBackend instance is enough for all hosts of that kind
                 backends[h] = shared.setdefault(type(b).__name__, b) if isinstance(b, StubBackend) else b
         self.backends = backends
@@ -75,6 +78,62 @@ class Daemon:
         self.services: list[Service] = []
         self._topology_cache: dict = {}
         self._lock = threading.Lock()
+        self.task_events: list[tuple[float, str, dict]] = []  # (unix time, host, event), newest last
+        self.events = None
+        self._start_task_events()
+
+    # ------------------------------------------------------------------ task-exit events
+    def _start_task_events(self) -> None:
+        """Task exits as events (core/events.py): a listener for the daemon's own node, the node
+        agents' event lines for remote nodes, the in-process hook of simulated nodes."""
+        from . import task_nursery
+        from .telemetry import RemoteBackend
+        from .transport import LocalTransport, SimulatedNode
+
+        if not getattr(self.cfg.launcher, "task_events", True):
+            return
+        local = [h for h, t in self.transports.transports.items() if isinstance(t, LocalTransport)]
+        if local:
+            from .events import EventListener
+
+            try:
+                self.events = EventListener(lambda ev: [self.on_task_event(h, ev) for h in local])
+            except OSError as e:
+                log.warning("task-exit events unavailable (%s); exits are found by polling", e)
+        for h, t in self.transports.transports.items():
+            if isinstance(t, SimulatedNode):
+                t.on_event = lambda ev, h=h: self.on_task_event(h, ev)
+        for h, b in self.backends.items():
+            if isinstance(b, RemoteBackend):
+                b.on_event = self.on_task_event
+        task_nursery.use_event_sockets(self.event_socket_for)
+
+    def event_socket_for(self, host: str) -> str | None:
+        """Where a task spawned on ``host`` reports its exit (``th-run --notify``)."""
+        from .telemetry import RemoteBackend
+        from .transport import LocalTransport
+
+        t = self.transports.transports.get(host)
+        if isinstance(t, LocalTransport):
+            return self.events.path if self.events is not None else None
+        b = self.backends.get(host)
+        if isinstance(b, RemoteBackend) and b.node_mode(host) == "agent" and b.stream_ms:
+            return self.cfg.launcher.node_events_socket or None
+        return None
+
+    def on_task_event(self, host: str, ev: dict) -> None:
+        """A task on ``host`` ended: refresh that host's telemetry now (its devices no longer show
+        the task's processes) and run the job scheduler, which releases the devices and starts the
+        next queued job in the same tick."""
+        with self._lock:
+            self.task_events.append((time.time(), host, dict(ev)))
+            del self.task_events[:-256]
+        from .services import MonitoringService
+
+        mon = self.service(MonitoringService)
+        if mon is not None and host in mon.backends:
+            mon.sample_host(host)
+        self.wake("task_exit")
 
     # ------------------------------------------------------------------ services
     def configure_services_from_config(self) -> list[Service]:
@@ -126,6 +185,9 @@ class Daemon:
     start = init
 
     def shutdown(self, timeout: float = 5.0) -> None:
+        if self.events is not None:
+            self.events.close()
+            self.events = None
         for s in self.services:
             s.stop()
         for s in self.services:
@@ -141,6 +203,8 @@ class Daemon:
 
         if task_nursery._transports is self.transports:
             task_nursery.use_transports(None)
+        if task_nursery._event_socket_for == self.event_socket_for:
+            task_nursery.use_event_sockets(None)
 
     def lookup_task_sessions(self, host: str, task_id: str) -> None:
         """Refresh the attestation registry for a claimed task it has not seen: list the task

@@ -67,6 +67,22 @@ def use_transports(tm: TransportManager | None) -> None:
     _transports = tm
 
 
+_event_socket_for = None  # host -> th-run --notify socket (core/events.py), set by the Daemon
+
+
+def use_event_sockets(fn) -> None:
+    global _event_socket_for
+    _event_socket_for = fn
+
+
+def _notify_path(host: str) -> str | None:
+    fn = _event_socket_for
+    try:
+        return fn(host) if fn is not None else None
+    except Exception:  # noqa: BLE001 -- events are an optimisation; spawning must not fail on them
+        return None
+
+
 def _client(host: str, user: str) -> TransportManager:
     return ssh.get_client(*ssh.build_dedicated_config_for(host, user))
 
@@ -80,9 +96,11 @@ def _run(host: str, user: str, cmd: str, timeout: float | None = None) -> Result
 
 
 def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | None = None,
-                        max_restarts: int = 0) -> str:
+                        max_restarts: int = 0, notify: str | None = None) -> str:
     name = session_name(task_id)
     logf = log_path(task_id)
+    # the task's exit is an event: th-run sends one datagram to this socket (core/events.py)
+    note = f" --notify {shlex.quote(notify)}" if notify else ""
     env = {"TENSORHIVE_TASK_ID": str(task_id), **(extra_env or {})}
     env_args = " ".join(f"--env {shlex.quote(f'{k}={v}')}" for k, v in env.items())
     th = shlex.quote(th_run)
@@ -91,7 +109,7 @@ def build_spawn_command(command: str, task_id, th_run: str, extra_env: dict | No
         policy = f" --max-restarts {int(max_restarts)} --restart-delay {get_config().launcher.restart_delay:g}"
     # th-run prints the task's pid; `status` then prints the new session's state (sid, uid, monitor
     # pid) in the same round trip, for core/attribution.py
-    primary = (f"{th} spawn --name {name} --log {logf} {env_args}{policy} -- bash -lc {shlex.quote(command)}"
+    primary = (f"{th} spawn --name {name} --log {logf}{note} {env_args}{policy} -- bash -lc {shlex.quote(command)}"
                f" && {th} status --name {name}")
     envs = " ".join(f"{k}={shlex.quote(str(v))}" for k, v in env.items())
     fallback = (f"mkdir -p $(dirname {logf}) && ( {envs} setsid bash -lc {shlex.quote(command)} "
@@ -143,7 +161,7 @@ def spawn(command: str, hostname: str, user: str, name_appendix: str = "", extra
           max_restarts: int = 0) -> int:
     env = {**spawn_env(hostname, command), **(extra_env or {})}
     r = _run(hostname, user, build_spawn_command(command, name_appendix, _th_run(hostname), env,
-                                                 max_restarts))
+                                                 max_restarts, _notify_path(hostname)))
     if r.exception is not None:
         raise SpawnError(f"connection failed: {r.exception}")
     pid = None

@@ -23,6 +23,7 @@ import ctypes
 import json
 import logging
 import math
+import shlex
 import os
 import subprocess
 import threading
@@ -410,6 +411,7 @@ class RemoteBackend(TelemetryBackend):
         self._started: dict[str, float] = {}
         self.errors: dict[str, str] = {}
         self._lock = threading.Lock()
+        self.on_event = None  # (host, event) -> None: task exits the node agent forwards (core/events.py)
 
     def node_mode(self, host: str) -> str:
         return self._modes.get(host, self.mode)
@@ -454,6 +456,14 @@ class RemoteBackend(TelemetryBackend):
                 if mode == "agent":
                     if doc.get("error"):
                         self.errors[host] = doc["error"]
+                        continue
+                    if doc.get("event") is not None:  # a task on the node exited (after a fresh entry)
+                        cb = self.on_event
+                        if cb is not None:
+                            try:
+                                cb(host, doc["event"])
+                            except Exception:  # noqa: BLE001
+                                log.exception("task event of %s failed", host)
                         continue
                     doc = doc.get("entry")
                     if doc is None:
@@ -594,19 +604,23 @@ class StubBackend(TelemetryBackend):
                                     for j in range(n)]} for i in range(n)]}
 
 
-def agent_args(probe: bool, probe_period: float, counters: bool, counters_period_ms: int, task_hbm: bool) -> str:
-    """The node agent's switches matching the daemon's ``[amd_monitor]`` settings."""
+def agent_args(probe: bool, probe_period: float, counters: bool, counters_period_ms: int, task_hbm: bool,
+               events_socket: str | None = None) -> str:
+    """The node agent's switches matching the daemon's ``[amd_monitor]`` settings (and the node's
+    task-exit socket, ``[launcher] node_events_socket``)."""
     a = ["--probe" if probe else "--no-probe", f"--probe-period {probe_period:g}",
          "--task-hbm" if task_hbm else "--no-task-hbm"]
     if counters:
         a += ["--counters", f"--counters-period-ms {int(counters_period_ms)}"]
+    if events_socket:
+        a += ["--events", shlex.quote(events_socket)]
     return " ".join(a)
 
 
 def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, probe: bool = False,
                  probe_period: float = 1.0, stream_ms: int | None = None, counters: bool = False,
                  counters_period_ms: int = 1000, task_hbm: bool = True, remote_mode: str = "agent",
-                 remote_agent: str = DEFAULT_AGENT) -> TelemetryBackend:
+                 remote_agent: str = DEFAULT_AGENT, events_socket: str | None = None) -> TelemetryBackend:
     """Pick a backend for ``host``: ``auto`` = amdsmi for the local node when /dev/kfd exists,
     remote th-smi for ssh nodes, stub otherwise."""
     spec_local = transports is None or getattr(transports.transports.get(host), "__class__", None).__name__ == "LocalTransport"
@@ -617,5 +631,6 @@ def make_backend(kind: str, host: str, transports=None, stub_gpus: int = 8, prob
                              counters_period_ms=counters_period_ms, task_hbm=task_hbm)
     if kind == "remote" or (kind == "auto" and not spec_local):
         return RemoteBackend(transports, stream_ms=stream_ms, mode=remote_mode, agent_cmd=remote_agent,
-                             agent_args=agent_args(probe, probe_period, counters, counters_period_ms, task_hbm))
+                             agent_args=agent_args(probe, probe_period, counters, counters_period_ms, task_hbm,
+                                                   events_socket))
     return StubBackend(stub_gpus)

@@ -175,7 +175,7 @@ class SimulatedNode(FakeTransport):
     GPUs named by ``HIP_VISIBLE_DEVICES`` with their owner and ``TENSORHIVE_TASK_ID``, exactly as
     the amdsmi backend would report them.  ``exit_task(pid)`` simulates a task finishing."""
 
-    _SPAWN = re.compile(r"spawn --name (\S+) --log (\S+)((?: --env \S+)*)(?: --max-restarts (\d+) --restart-delay \S+)?"
+    _SPAWN = re.compile(r"spawn --name (\S+) --log (\S+)(?: --notify \S+)?((?: --env \S+)*)(?: --max-restarts (\d+) --restart-delay \S+)?"
                         r" -- bash -lc (.*?)(?: && \S+ status --name \S+)?; else")
     _SIG = re.compile(r"then \S+ (interrupt|terminate|kill) --pid (\d+)")
 
@@ -188,6 +188,7 @@ class SimulatedNode(FakeTransport):
         self.tty_messages: list[tuple[str, str]] = []  # (tty, text) written by warnings
         self.killed: list[tuple[int, str | None, bool]] = []  # (pid, as user, via sudo)
         self._next = first_pid
+        self.on_event = None  # th-run's task-exit notification (the Daemon's on_task_event)
 
     def run(self, command, timeout=None, user=None, env=None) -> Result:
         with self._lock:
@@ -277,7 +278,7 @@ class SimulatedNode(FakeTransport):
         if s is None:
             return None
         if s["restarts"] >= s["max_restarts"]:
-            self.exit_task(pid, f"[simulated] exit code {code}")
+            self.exit_task(pid, f"[simulated] exit code {code}", code=code)
             return None
         self._drop_gpu_process(pid)
         with self._lock:
@@ -296,13 +297,16 @@ class SimulatedNode(FakeTransport):
                                            ancestors=[s["monitor_pid"]])
         return new
 
-    def exit_task(self, pid: int, line: str = "[simulated] done") -> None:
+    def exit_task(self, pid: int, line: str = "[simulated] done", code: int = 0) -> None:
         with self._lock:
             s = self.sessions.pop(pid, None)
         if s is None:
             return
         self.logs.setdefault(s["log"], []).append(line)
         self._drop_gpu_process(pid)
+        if self.on_event is not None:  # like th-run: after the state says exited
+            self.on_event({"event": "task_exit", "name": s["name"], "pid": pid, "exit_code": code,
+                           "ended_ms": int(time.time() * 1000)})
 
     def _signal(self, pid: int, verb: str, user) -> Result:
         with self._lock:

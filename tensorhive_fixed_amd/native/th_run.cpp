@@ -5,14 +5,17 @@
 // and controlled with `screen -X stuff ^C` / `screen -X quit` / `kill -9` / `screen -ls`.
 //
 //   th-run spawn --name NAME --log FILE [--state-dir DIR] [--env K=V]... [--cwd DIR]
-//                [--max-restarts N] [--restart-delay S] -- CMD ARGS...
+//                [--max-restarts N] [--restart-delay S] [--notify SOCK] -- CMD ARGS...
 //       Detaches (double fork + setsid), starts CMD in its OWN process group with stdout+stderr
 //       on a pipe, and prints the pid of CMD (== its pgid) on stdout, then returns.  A small
 //       monitor process (own session, ignores SIGINT/SIGTERM/SIGHUP like `tee --ignore-interrupts`)
 //       copies the pipe into FILE line by line, reaps CMD and records its exit status.  With
 //       --max-restarts N a run that exits non-zero is started again (new pid/pgid, same log,
 //       TH_RUN_RESTART=k in its env) up to N times, unless the stop was requested through th-run
-//       (SURVEY §5 failure row: restart policy; the reference only detects failures).
+//       (SURVEY §5 failure row: restart policy; the reference only detects failures).  With
+//       --notify SOCK (or $TH_RUN_NOTIFY) the monitor sends one datagram to that unix socket when
+//       the task has exited and its state says so: the daemon's scheduler wakes on the event
+//       instead of discovering the exit by polling (core/events.py).
 //   th-run interrupt|terminate|kill (--name NAME | --pid PID) [--state-dir DIR]
 //       SIGINT / SIGTERM / SIGKILL to the task's whole process group (torchrun + all ranks).
 //   th-run ls [--all] [--state-dir DIR]     one JSON object per session (live ones by default)
@@ -33,8 +36,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <sys/un.h>
 #include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
@@ -151,7 +156,8 @@ std::string to_json(const KV& kv, bool alive) {
     const bool num = it.first == "pid" || it.first == "pgid" || it.first == "monitor_pid" ||
                      it.first == "exit_code" || it.first == "started" || it.first == "ended" ||
                      it.first == "first_pid" || it.first == "restarts" || it.first == "max_restarts" ||
-                     it.first == "last_exit_code" || it.first == "sid" || it.first == "uid";
+                     it.first == "last_exit_code" || it.first == "sid" || it.first == "uid" ||
+                     it.first == "ended_ms";
     o += "\"" + json_escape(it.first) + "\":";
     if (num && !it.second.empty())
       o += it.second;
@@ -160,6 +166,35 @@ std::string to_json(const KV& kv, bool alive) {
   }
   o += std::string(first ? "" : ",") + "\"alive\":" + (alive ? "true" : "false") + "}";
   return o;
+}
+
+long long now_ms() {
+  struct timespec t;
+  clock_gettime(CLOCK_REALTIME, &t);
+  return (long long)t.tv_sec * 1000 + t.tv_nsec / 1000000;
+}
+
+// Task-exit event: one datagram to the daemon's (or the node agent's) unix socket, sent after the
+// state file says `exited`, so whoever wakes on it reads the final state (core/events.py).  A hint
+// only: a missing or full socket loses nothing but latency (the daemon still polls).
+void notify_event(const std::string& path, const KV& st) {
+  if (path.empty() || path.size() >= sizeof(((struct sockaddr_un*)nullptr)->sun_path)) return;
+  int fd = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return;
+  struct sockaddr_un a;
+  memset(&a, 0, sizeof a);
+  a.sun_family = AF_UNIX;
+  memcpy(a.sun_path, path.c_str(), path.size());
+  std::string msg = "{\"event\":\"task_exit\"";
+  for (const char* k : {"name", "pid", "exit_code", "restarts", "ended_ms", "user"}) {
+    auto it = st.find(k);
+    if (it == st.end()) continue;
+    const bool num = strcmp(k, "name") != 0 && strcmp(k, "user") != 0;
+    msg += std::string(",\"") + k + "\":" + (num ? it->second : "\"" + json_escape(it->second) + "\"");
+  }
+  msg += "}";
+  (void)sendto(fd, msg.data(), msg.size(), MSG_DONTWAIT, (struct sockaddr*)&a, sizeof a);
+  close(fd);
 }
 
 void write_all(int fd, const char* p, ssize_t n) {
@@ -177,14 +212,14 @@ void write_all(int fd, const char* p, ssize_t n) {
 int usage() {
   fprintf(stderr,
           "usage: th-run spawn --name NAME --log FILE [--state-dir D] [--env K=V].. [--cwd D]\n"
-          "                    [--max-restarts N] [--restart-delay S] -- CMD..\n"
+          "                    [--max-restarts N] [--restart-delay S] [--notify SOCK] -- CMD..\n"
           "       th-run interrupt|terminate|kill (--name NAME | --pid PID) [--state-dir D]\n"
           "       th-run ls [--all] [--state-dir D] | status --name NAME | wait --name NAME [--timeout S]\n");
   return 2;
 }
 
 struct Args {
-  std::string cmd, name, log, state_dir, cwd;
+  std::string cmd, name, log, state_dir, cwd, notify;
   long pid = -1;
   double timeout = -1, restart_delay = 1.0;
   int max_restarts = 0;
@@ -197,6 +232,7 @@ bool parse(int argc, char** argv, Args& a) {
   if (argc < 2) return false;
   a.cmd = argv[1];
   a.state_dir = state_dir_default();
+  if (const char* n = getenv("TH_RUN_NOTIFY")) a.notify = n;
   for (int i = 2; i < argc; ++i) {
     std::string s = argv[i];
     auto need = [&](std::string& dst) {
@@ -215,6 +251,8 @@ bool parse(int argc, char** argv, Args& a) {
       if (!need(a.state_dir)) return false;
     } else if (s == "--cwd") {
       if (!need(a.cwd)) return false;
+    } else if (s == "--notify") {
+      if (!need(a.notify)) return false;
     } else if (s == "--env") {
       std::string e;
       if (!need(e)) return false;
@@ -299,6 +337,7 @@ int do_spawn(Args& a) {
   for (auto& s : a.argv) cmdline += (cmdline.empty() ? "" : " ") + s;
   st["cmd"] = cmdline;
   st["max_restarts"] = std::to_string(a.max_restarts);
+  if (!a.notify.empty()) st["notify"] = a.notify;
   // Attestation of the task's processes (core/attribution.py): every process the task starts is
   // in THIS session (the first child's setsid above) unless it calls setsid itself, and then its
   // parent chain still reaches this monitor.  Neither can be joined by a process started outside
@@ -408,7 +447,9 @@ int do_spawn(Args& a) {
   st["exit_code"] = std::to_string(code);
   st["restarts"] = std::to_string(restarts);
   st["ended"] = std::to_string((long)time(nullptr));
+  st["ended_ms"] = std::to_string(now_ms());
   write_state(a.state_dir, a.name, st);
+  notify_event(a.notify, st);
   unlink(stopf.c_str());
   close(logfd);
   _exit(0);
