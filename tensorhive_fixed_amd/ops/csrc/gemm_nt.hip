@@ -61,6 +61,15 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16
 
 __device__ __forceinline__ bf16x8 lds_rd(const char LDS_AS* p) { return *reinterpret_cast<const bf16x8 LDS_AS*>(p); }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N), fully expanded
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_nt(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_nt<I + 1, N>(f);
+  }
+}
+
 // fragment read order of a phase: the next phase starts with block row 0 (A0 against B0..B7)
 __device__ constexpr int RD_ORDER[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};  // <8: A, else B
 
@@ -402,6 +411,195 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_nt_kernel(const ushort* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Schedule "hb" (launch flags bit 5): the same machine (256 x 256 x 64, 4 waves of 128 x 128,
+// 16x16x32, 256 AGPR accumulators, 2-stage 128 KB ring) with ONE k-tile per loop iteration and the
+// synchronisation split per operand, so the DMA of a tile never has to be waited for with vmcnt(0):
+//   MFMA   0- 63  k-step 0 of tile t (fragments X, read at the end of the previous iteration)
+//           1- 15  read A's k-step-1 fragments of tile t (Y.a)       | 20: lgkmcnt(0) + barrier: every
+//          22- 36  DMA A of tile t+2 into tile t's stage               |     wave is done with A of tile t
+//          25- 39  read B's k-step-1 fragments (Y.b)                   | 48: lgkmcnt(0) + barrier
+//          50- 66  DMA B pieces 0-4 of tile t+2 (13 pieces issued)
+//   MFMA  64-127  k-step 1 of tile t (Y)
+//          80      vmcnt(13): the previous iteration's 16 pieces (tile t+1) landed; barrier
+//          84-116  DMA B pieces 5-7; 94-124 read tile t+1's k-step-0 fragments (X) from the other stage
+// Each DMA has about one iteration of lead time and is waited for by count; the barriers release
+// each operand region as soon as its last reader is past it.  DMA pieces are buffer_load ... lds
+// with the k-tile in the descriptor base and a loop-invariant soffset per piece (two instructions
+// per piece).  SV bit0: reads of X spread one per 3 MFMAs from 82 (with bit1: the tile-(t+1) wait at
+// 72 and the reads one per 2 MFMAs from 74);
+// SV bit1: B's reads at 17-31, its barrier at 38 and ALL its DMA pieces at 40-68, so the tile-(t+1)
+// wait at 88 is vmcnt(16) (every piece has > 1 iteration of lead time).
+template <int SV>
+__global__ __launch_bounds__(NTHR, 1) void gemm_nt_hb_kernel(const ushort* __restrict__ A, long lda,
+                                                            const ushort* __restrict__ B, long ldb,
+                                                            ushort* __restrict__ C, long ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(1024))) char smem_raw[SMEM];
+  const int nM = M / BM, nN = N / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int per_band = GM * nN;
+  const int band = L / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = L % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int r16 = lane & 15, g = lane >> 4;
+  const char LDS_AS* smem = (const char LDS_AS*)smem_raw;
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem_raw;
+  int rd[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) rd[k] = r16 * 128 + (((4 * k + g) ^ (r16 >> 1)) << 4);
+  const int a_wave = wr * 128 * 128, b_wave = wc * 128 * 128;
+  const int dma_row = w * 64;  // wave w stages image rows [64 w, 64 w + 64) of A and of B
+  const ushort* ga = A + (m0 + dma_row) * lda;
+  const ushort* gb = B + (n0 + dma_row) * ldb;
+  // lane -> row (lane >> 3) of a piece, slot (lane & 7) holding global chunk slot ^ (4 (p & 1) + (lane >> 4))
+  unsigned va[2], vb[2];
+  {
+    const int rr = lane >> 3, slot = lane & 7;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int chunk = slot ^ (4 * par + (lane >> 4));
+      va[par] = (unsigned)(2 * ((long)rr * lda + 8 * chunk));
+      vb[par] = (unsigned)(2 * ((long)rr * ldb + 8 * chunk));
+    }
+  }
+  const unsigned lds_wave = lds0 + dma_row * 128;
+  const unsigned sa_step = (unsigned)(2L * 8 * lda), sb_step = (unsigned)(2L * 8 * ldb);  // bytes per piece (8 rows)
+  // piece p of operand X (0 = A, 1 = B) of k-tile kt into stage st
+  auto piece = [&](int op, int p, int kt, int st) {
+    const ushort* base = (op == 0 ? ga : gb) + (long)kt * BK;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    const unsigned soff = (unsigned)p * (op == 0 ? sa_step : sb_step);
+    const unsigned voff = op == 0 ? va[p & 1] : vb[p & 1];
+    const unsigned lb = __builtin_amdgcn_readfirstlane(lds_wave + st * STAGE + op * IMG + p * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(lb), "v"(voff), "s"(r), "s"(soff) : "memory", "m0");
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.f);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4" ::);
+
+  const int nt = K / BK;
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) piece(0, p, 0, 0);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) piece(1, p, 0, 0);
+  const int kt1 = min(1, nt - 1);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) piece(0, p, kt1, 1);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) piece(1, p, kt1, 1);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  {
+    const char LDS_AS* sa = smem + a_wave + rd[0];
+    const char LDS_AS* sb = smem + IMG + b_wave + rd[0];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      xa[f] = lds_rd(sa + f * 2048);
+      xb[f] = lds_rd(sb + f * 2048);
+    }
+  }
+  for (int t = 0; t < nt; ++t) {
+    const int st = t & 1;
+    const int kt2 = min(t + 2, nt - 1);  // past the end: re-stage the last tile (nobody reads it)
+    const char LDS_AS* sa1 = smem + st * STAGE + a_wave + rd[1];
+    const char LDS_AS* sb1 = smem + st * STAGE + IMG + b_wave + rd[1];
+    const char LDS_AS* sa0 = smem + (st ^ 1) * STAGE + a_wave + rd[0];
+    const char LDS_AS* sb0 = smem + (st ^ 1) * STAGE + IMG + b_wave + rd[0];
+    static_for_nt<0, 128>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      constexpr int mm = m & 63, i = mm >> 3, j = mm & 7;
+      if constexpr (m < 64)
+        mfma_acc(acc[i][j], xb[j], xa[i]);
+      else
+        mfma_acc(acc[i][j], yb[j], ya[i]);
+      if constexpr (m >= 1 && m <= 15 && (m & 1)) ya[(m - 1) / 2] = lds_rd(sa1 + ((m - 1) / 2) * 2048);
+      if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (m >= 22 && m <= 36 && !(m & 1)) piece(0, (m - 22) / 2, kt2, st);
+      if constexpr (SV & 2) {
+        // every B piece before the tile-(t+1) wait, which then lets all 16 of this tile fly (vmcnt(16))
+        if constexpr (m >= 17 && m <= 31 && (m & 1)) yb[(m - 17) / 2] = lds_rd(sb1 + ((m - 17) / 2) * 2048);
+        if constexpr (m == 38) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (m >= 40 && m <= 68 && ((m - 40) % 4 == 0)) piece(1, (m - 40) / 4, kt2, st);
+        if constexpr (m == ((SV & 1) ? 72 : 88)) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+      } else {
+        if constexpr (m >= 25 && m <= 39 && (m & 1)) yb[(m - 25) / 2] = lds_rd(sb1 + ((m - 25) / 2) * 2048);
+        if constexpr (m == 48) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (m >= 50 && m <= 66 && ((m - 50) % 4 == 0)) piece(1, (m - 50) / 4, kt2, st);
+        if constexpr (m == 80) asm volatile("s_waitcnt vmcnt(13)\n\ts_barrier" ::: "memory");
+        if constexpr (m == 84 || m == 100 || m == 116) piece(1, 5 + (m - 84) / 16, kt2, st);
+      }
+      if constexpr (SV & 1) {
+        constexpr int X1 = (SV & 2) ? 74 : 82;
+        if constexpr (m >= X1 && m <= 127 && ((m - X1) % 2 == 0) && (m - X1) / 2 < 16 && (SV & 2)) {
+          constexpr int f = (m - X1) / 2;
+          if constexpr (f < 8) xa[f] = lds_rd(sa0 + f * 2048);
+          else xb[f - 8] = lds_rd(sb0 + (f - 8) * 2048);
+        }
+        if constexpr (m >= 82 && m <= 127 && ((m - 82) % 3 == 0) && (m - 82) / 3 < 16 && !(SV & 2)) {
+          constexpr int f = (m - 82) / 3;
+          if constexpr (f < 8) xa[f] = lds_rd(sa0 + f * 2048);
+          else xb[f - 8] = lds_rd(sb0 + (f - 8) * 2048);
+        }
+      } else {
+        constexpr int X0 = (SV & 2) ? 90 : 94;
+        if constexpr (m >= X0 && m <= X0 + 30 && !(m & 1)) {
+          constexpr int f = (m - X0) / 2;  // A0 B0..B7 first: the next iteration starts with row 0
+          constexpr int ord[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};
+          constexpr int q = ord[f];
+          if constexpr (q < 8) xa[q] = lds_rd(sa0 + q * 2048);
+          else xb[q - 8] = lds_rd(sb0 + (q - 8) * 2048);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  // epilogue (as gemm_nt_kernel): stage the wave's 128 x 128 bf16 tile in LDS, then 16-B row stores
+  char LDS_AS* ep = (char LDS_AS*)smem_raw + w * 32768;
+  const long crow0 = m0 + wr * 128, ccol0 = n0 + wc * 128;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 v = acc[i][j];
+      ushort4v o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      const int row = 16 * i + r16;
+      const int blk = (2 * j + (g >> 1)) ^ r16;
+      *reinterpret_cast<ushort4v LDS_AS*>(ep + row * 256 + blk * 16 + (g & 1) * 8) = o;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const int row = 4 * q + g;
+    const ushort8 v = *reinterpret_cast<const ushort8 LDS_AS*>(ep + row * 256 + ((r16 ^ (row & 15)) << 4));
+    *reinterpret_cast<ushort8*>(C + (crow0 + row) * ldc + ccol0 + 8 * r16) = v;
+  }
+}
+
 extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                           int beta, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
@@ -414,6 +612,20 @@ extern "C" int th_gemm_nt(const void* A, long lda, const void* B, long ldb, void
 #define TH_NT_LAUNCH(BT, V)                                                                                 \
   gemm_nt_kernel<BT, V><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, \
                                                        M, N, K)
+  if (!beta && (flags & 32)) {  // schedule "hb" (gemm_nt_hb_kernel), sub-variant SV in bits 6-7
+    // buffer descriptors address the operands from this workgroup's first staged row: 32-bit offsets
+    if ((long)K * 2 + 256L * 2 * max(lda, ldb) >= (1L << 31)) return -1;
+#define TH_NT_HB(SV_) \
+  gemm_nt_hb_kernel<SV_><<<(unsigned)grid, NTHR, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, M, N, K)
+    switch ((flags >> 6) & 3) {
+      case 1: TH_NT_HB(1); break;
+      case 2: TH_NT_HB(2); break;
+      case 3: TH_NT_HB(3); break;
+      default: TH_NT_HB(0); break;
+    }
+#undef TH_NT_HB
+    TH_CHECK_LAUNCH();
+  }
   // flags bits 0-4: schedule variant (see gemm_nt_kernel); beta = 1 runs the default schedule
   switch (beta ? 64 : (flags & 31)) {
     case 1: TH_NT_LAUNCH(false, 1); break;

@@ -70,6 +70,14 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N), fully expanded
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_tn(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_tn<I + 1, N>(f);
+  }
+}
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -732,6 +740,215 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_tn_w4_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Schedule "hb" (launch flags bit 6): one wave per SIMD, the machine of hipBLASLt's NT kernels and of
+// ops/csrc/gemm_nt.hip's hb schedule, on the TN operands:
+//   * tile 256 x 256 x 64, 4 waves as 2 (M) x 2 (N), wave tile 128 x 128 = 8 x 8 blocks of
+//     v_mfma_f32_16x16x32_bf16 -> 64 f32x4 accumulators pinned in the 256 AGPRs by inline-asm MFMAs;
+//   * per stage an A and a B image of 64 k-rows x 512 B (2-stage ring, 128 KB), k-row r's 64-B chunk c
+//     at c ^ S(r), S(r) = (r + (r >> 3)) & 3 (the pp2 SW swizzle: both transposed reads of a 16x16x32
+//     operand, rows 8 apart, conflict-free); an operand is one tr_pair (two ds_read_b64_tr_b16);
+//   * DMA as buffer_load ... lds: the k-tile in the descriptor base, one loop-invariant soffset per
+//     piece (2 k-rows = 1 KB), the lane's swizzled chunk in the voffset (4 per operand);
+//   * one k-tile per iteration, synchronisation split per operand (see gemm_nt_hb_kernel):
+//       MFMA   0- 63  k-step 0 (fragments X);  0-15 read A's k-step-1 fragments (16 tr reads) | 20 barrier
+//              22- 36 DMA A of tile t+2 (8 pieces);  23-38 read B's k-step-1 fragments       | 44 barrier
+//              46- 74 DMA B of tile t+2 (8 pieces, every 4th MFMA)
+//       MFMA  64-127  k-step 1 (Y); 88: vmcnt(16) + barrier (tile t+1 landed); 90-121 read X of tile t+1
+//   * epilogue: bf16 through LDS with 16-B row stores (beta: C added), or f32x4 stores into the split-K slab.
+template <bool SPLIT, bool BETA>
+__global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
+    const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk) {
+  constexpr int HIMG = 64 * ROWB;     // 32 KB: 64 k-rows x 256 columns
+  constexpr int HSTAGE = 2 * HIMG;    // A | B
+  __shared__ __attribute__((aligned(1024))) char smem_raw[2 * HSTAGE];
+  const char LDS_AS* smem = (const char LDS_AS*)smem_raw;
+  const int nM = M / TM, nN = N / TN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = SPLIT ? L / splitk : L;
+  const int split = SPLIT ? L % splitk : 0;
+  constexpr int GM = TH_TN_GM;
+  const int per_band = GM * nN;
+  const int band = tile / per_band;
+  const int first_m = band * GM;
+  const int gm = min(GM, nM - first_m);
+  const int in_band = tile % per_band;
+  const int tm = first_m + in_band % gm;
+  const int tn = in_band / gm;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const int kper = K / splitk;
+  const long kbeg = (long)split * kper;
+  const int nt = kper / 64;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  // transposed-read offsets (16x16x32 operand of lane l: column l & 15 of a 16-column block, k rows
+  // 8 (l >> 4) .. +7 as rows 8g + q and 8g + 4 + q, columns 4p .. 4p + 3 of each b64 half)
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lane_base16 = (8 * g + q) * ROWB + 8 * p;
+  const int x16 = (q + g) & 3;
+  int a_off[8], b_off[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    const int ca = wm * 128 + 16 * f, cb = wn * 128 + 16 * f;
+    a_off[f] = lane_base16 + (((ca >> 5) ^ x16) << 6) + (ca & 31) * 2;
+    b_off[f] = lane_base16 + (((cb >> 5) ^ x16) << 6) + (cb & 31) * 2;
+  }
+  // DMA: piece u = 4 i + w (i = 0..7) of an operand writes k-rows 2u, 2u + 1 (lane half hi); the
+  // lane's global chunk is slot ^ S(row), S(row) = (2 w + hi + i) & 3 -> one voffset per i & 3
+  const int hi = lane >> 5, slot = lane & 31;
+  unsigned va[4], vb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = (slot >> 2) ^ ((2 * w + hi + i) & 3);
+    va[i] = (unsigned)(2 * ((long)hi * lda + chunk * 32 + (slot & 3) * 8));
+    vb[i] = (unsigned)(2 * ((long)hi * ldb + chunk * 32 + (slot & 3) * 8));
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem_raw;
+  const ushort* ga = A + kbeg * lda + m0;
+  const ushort* gb = B + kbeg * ldb + n0;
+  auto piece = [&](int op, int i, int kt, int st) {
+    const long ld = op == 0 ? lda : ldb;
+    const ushort* base = (op == 0 ? ga : gb) + (long)kt * 64 * ld;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    const int u = 4 * i + w;
+    const unsigned soff = (unsigned)(2L * 2 * u * ld);
+    const unsigned voff = op == 0 ? va[i & 3] : vb[i & 3];
+    const unsigned lb = __builtin_amdgcn_readfirstlane(lds0 + st * HSTAGE + op * HIMG + u * 1024);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(lb), "v"(voff), "s"(r), "s"(soff) : "memory", "m0");
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.f);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_nop 4" ::);
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) piece(0, i, 0, 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) piece(1, i, 0, 0);
+  const int kt1 = min(1, nt - 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) piece(0, i, kt1, 1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) piece(1, i, kt1, 1);
+  asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    xa[f] = tr_pair(smem + a_off[f], smem + a_off[f] + 4 * ROWB);
+    xb[f] = tr_pair(smem + HIMG + b_off[f], smem + HIMG + b_off[f] + 4 * ROWB);
+  }
+  auto mf = [&](f32x4& c, const bf16x8& b, const bf16x8& a) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+  };
+  // one transposed b64 half of fragment f (0-7 A, 8-15 B) of k-step ks, stage base sb
+  auto rd_half = [&](const char LDS_AS* sb, int f, int ks, int half) -> i16x4 {
+    const int off = (f < 8 ? a_off[f] : HIMG + b_off[f - 8]) + ks * 32 * ROWB + half * 4 * ROWB;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(sb + off));
+  };
+  auto join = [](i16x4 lo, i16x4 hi2) {
+    typedef short i16x8 __attribute__((ext_vector_type(8)));
+    const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi2[0], hi2[1], hi2[2], hi2[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  i16x4 lo_y = {0, 0, 0, 0}, lo_x = {0, 0, 0, 0};
+  for (int t = 0; t < nt; ++t) {
+    const int st = t & 1;
+    const int kt2 = min(t + 2, nt - 1);  // past the end: re-stage the last tile (nobody reads it)
+    const char LDS_AS* s_cur = smem + st * HSTAGE;
+    const char LDS_AS* s_nxt = smem + (st ^ 1) * HSTAGE;
+    static_for_tn<0, 128>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      constexpr int mm = m & 63, i = mm >> 3, j = mm & 7;
+      if constexpr (m < 64)
+        mf(acc[i][j], xb[j], xa[i]);
+      else
+        mf(acc[i][j], yb[j], ya[i]);
+      // Y.a: 16 halves at MFMAs 0-15
+      if constexpr (m < 16) {
+        if constexpr (!(m & 1)) lo_y = rd_half(s_cur, m >> 1, 1, 0);
+        else ya[m >> 1] = join(lo_y, rd_half(s_cur, m >> 1, 1, 1));
+      }
+      if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (m >= 22 && m <= 36 && !(m & 1)) piece(0, (m - 22) / 2, kt2, st);
+      // Y.b: 16 halves at MFMAs 23-38
+      if constexpr (m >= 23 && m <= 38) {
+        constexpr int h = m - 23;
+        if constexpr (!(h & 1)) lo_y = rd_half(s_cur, 8 + (h >> 1), 1, 0);
+        else yb[h >> 1] = join(lo_y, rd_half(s_cur, 8 + (h >> 1), 1, 1));
+      }
+      if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (m >= 46 && m <= 74 && ((m - 46) % 4 == 0)) piece(1, (m - 46) / 4, kt2, st);
+      if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+      // X of tile t+1: 32 halves at MFMAs 90-121, A0 B0-B7 A1-A7 (the next iteration starts with row 0)
+      if constexpr (m >= 90 && m <= 121) {
+        constexpr int h = m - 90;
+        constexpr int ord[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};
+        constexpr int f = ord[h >> 1];
+        if constexpr (!(h & 1)) {
+          lo_x = rd_half(s_nxt, f, 0, 0);
+        } else {
+          const bf16x8 v = join(lo_x, rd_half(s_nxt, f, 0, 1));
+          if constexpr (f < 8) xa[f] = v;
+          else xb[f - 8] = v;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  // lane holds C[m = 16 i + r16][n = 16 j + 4 g4 .. +3] of the wave tile
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const long crow0 = m0 + wm * 128, ccol0 = n0 + wn * 128;
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        *reinterpret_cast<f32x4*>(slab + ((long)split * M + crow0 + 16 * i + r16) * N + ccol0 + 16 * j + 4 * g4) = acc[i][j];
+    return;
+  }
+  char LDS_AS* ep = (char LDS_AS*)smem_raw + w * 32768;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f32x4 v = acc[i][j];
+      if constexpr (BETA) {
+        const ushort4v old = *reinterpret_cast<const ushort4v*>(C + (crow0 + 16 * i + r16) * ldc + ccol0 + 16 * j + 4 * g4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bf2f(old[e]);
+      }
+      ushort4v o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      const int row = 16 * i + r16;
+      const int blk = (2 * j + (g4 >> 1)) ^ r16;
+      *reinterpret_cast<ushort4v LDS_AS*>(ep + row * 256 + blk * 16 + (g4 & 1) * 8) = o;
+    }
+  }
+#pragma unroll
+  for (int qq = 0; qq < 32; ++qq) {
+    const int row = 4 * qq + g4;
+    const ushort8 v = *reinterpret_cast<const ushort8 LDS_AS*>(ep + row * 256 + ((r16 ^ (row & 15)) << 4));
+    *reinterpret_cast<ushort8*>(C + (crow0 + row) * ldc + ccol0 + 8 * r16) = v;
+  }
+}
+
 // C[m][n] (+)= sum over splits of slab[s][m][n], 8 elements per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
                                                              long ldc, int M, int N, int splitk, int beta) {
@@ -772,7 +989,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 //        bit2 (with bit1) = DMA three k-tiles ahead;
 //        bit3 = one wave per SIMD, 128 x 128 per wave (gemm_tn_w4_kernel, 256 threads);
 //        bit4 (with bit1) = v_mfma_f32_16x16x32_bf16 fragments in the ping-pong v2 kernel;
-//        bit5 (with bit1) = row swizzle S(r) = (r + (r >> 3)) & 3 of the v2 images
+//        bit5 (with bit1) = row swizzle S(r) = (r + (r >> 3)) & 3 of the v2 images;
+//        bit6 = schedule "hb" (gemm_tn_hb_kernel: one wave per SIMD, 16x16x32 asm MFMAs, per-operand barriers)
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -805,7 +1023,14 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
     } else if (splitk > 1) KERNEL<true, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta); \
     else KERNEL<false, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
   } while (0)
-  if (flags & 8) {
+  if (flags & 64) {  // schedule "hb": one wave per SIMD, 64-deep k-tiles
+    if (K / splitk < 64 || (K / splitk) % 64) return -1;
+    // buffer descriptors per k-tile: 32-bit offsets over 64 k-rows of one operand
+    if (2L * 64 * max(lda, ldb) + 512 >= (1L << 31)) return -1;
+    if (splitk > 1) gemm_tn_hb_kernel<true, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk);
+    else if (beta) gemm_tn_hb_kernel<false, true><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1);
+    else gemm_tn_hb_kernel<false, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1);
+  } else if (flags & 8) {
     if (splitk > 1) gemm_tn_w4_kernel<true><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta);
     else gemm_tn_w4_kernel<false><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);
   } else if (pp2 && (flags & 4)) TH_TN_LAUNCH2(gemm_tn_pp2_kernel, 3);

@@ -50,7 +50,7 @@ def gemm_nt_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
             torch.mm(a, b.t(), out=out)
         return out
     _lib.call("th_gemm_nt", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), _VARIANT if variant is None else int(variant) & 31, _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), _VARIANT if variant is None else int(variant) & 127, _lib.stream_ptr(a.device))
     return out
 
 
