@@ -57,3 +57,17 @@ def mm_into(a: torch.Tensor, b: torch.Tensor) -> Callable[[torch.Tensor, bool], 
             torch.mm(a, b, out=o2)
 
     return _w
+
+
+def nt_mm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``a @ b.t()`` (into ``out`` when given): the K-contiguous ("NT") form of the forward and
+    input-gradient GEMMs, on hipBLASLt.  (The hand-written NT kernel reached 0.93-0.96x of it at
+    K = 4096 and 0.84x at large K and was removed: profiles/r05_gemm/.)"""
+    if out is not None:
+        return torch.mm(a, b.t(), out=out)
+    return torch.mm(a, b.t())
+
+
+def nt_into(a: torch.Tensor, b: torch.Tensor) -> Callable[[torch.Tensor, bool], None]:
+    """A ``write`` callback computing ``a @ b.t()`` (hipBLASLt)."""
+    return mm_into(a, b.t())

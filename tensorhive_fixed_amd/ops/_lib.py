@@ -48,7 +48,6 @@ _SIGS: dict[str, list] = {
     "th_embedding_bwd": [P, P, P, P, L, I, I, P],
     "th_transpose_bf16": [P, P, L, L, L, I, P],
     "th_gemm_tn": [P, L, P, L, P, L, I, I, I, I, I, P, I, P],
-    "th_gemm_nt": [P, L, P, L, P, L, I, I, I, I, I, P],
 }
 
 

@@ -15,8 +15,8 @@ import os
 import torch
 
 from . import _lib
+from ._grad import nt_mm
 from .gemm_tn import gemm_tn_, supported as gemm_tn_supported
-from .gemm_nt import nt_mm
 from .linear import _DGRAD_NT
 from .transpose import transpose
 

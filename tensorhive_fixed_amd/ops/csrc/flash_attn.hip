@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_kh_kernel(
 // kh splits each 32-key slice between a dK and a dV wave because one wave cannot hold both
 // accumulator sets beside its operands in 256 registers.  Here the dK^T and dV^T accumulators
 // (8 x f32x16 = 128 registers) sit in the AGPR half of the 512-entry file, pinned there by
-// inline-asm MFMAs ("+a" operands, as in ops/csrc/gemm_nt.hip), so ONE wave computes S, P, dP, dS,
+// inline-asm MFMAs ("+a" operands, as in gemm_tn.hip's hb kernel), so ONE wave computes S, P, dP, dS,
 // dV^T and dK^T of its 32 keys:
 //   * no P exchange through LDS and one barrier per tile (kh: two);
 //   * 4 waves cover 128 keys per staged Q|dO tile (kh: 64), so half the LDS-DMA bytes per MFMA;

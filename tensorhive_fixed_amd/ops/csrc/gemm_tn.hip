@@ -742,7 +742,8 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_tn_w4_kernel(
 
 // ---------------------------------------------------------------------------------------------
 // Schedule "hb" (launch flags bit 6): one wave per SIMD, the machine of hipBLASLt's NT kernels and of
-// ops/csrc/gemm_nt.hip's hb schedule, on the TN operands:
+// the NT kernel's hb schedule (removed in round 5: profiles/r05_gemm/gemm_nt_removed.patch), on the
+// TN operands:
 //   * tile 256 x 256 x 64, 4 waves as 2 (M) x 2 (N), wave tile 128 x 128 = 8 x 8 blocks of
 //     v_mfma_f32_16x16x32_bf16 -> 64 f32x4 accumulators pinned in the 256 AGPRs by inline-asm MFMAs;
 //   * per stage an A and a B image of 64 k-rows x 512 B (2-stage ring, 128 KB), k-row r's 64-B chunk c
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_tn_w4_kernel(
 //     operand, rows 8 apart, conflict-free); an operand is one tr_pair (two ds_read_b64_tr_b16);
 //   * DMA as buffer_load ... lds: the k-tile in the descriptor base, one loop-invariant soffset per
 //     piece (2 k-rows = 1 KB), the lane's swizzled chunk in the voffset (4 per operand);
-//   * one k-tile per iteration, synchronisation split per operand (see gemm_nt_hb_kernel):
+//   * one k-tile per iteration, synchronisation split per operand (released per operand, as in hipBLASLt's loop):
 //       MFMA   0- 63  k-step 0 (fragments X);  0-15 read A's k-step-1 fragments (16 tr reads) | 20 barrier
 //              22- 36 DMA A of tile t+2 (8 pieces);  23-38 read B's k-step-1 fragments       | 44 barrier
 //              46- 74 DMA B of tile t+2 (8 pieces, every 4th MFMA)

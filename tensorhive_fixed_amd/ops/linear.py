@@ -26,8 +26,7 @@ import os
 
 import torch
 
-from ._grad import deliver, mm_into
-from .gemm_nt import nt_into, nt_mm
+from ._grad import deliver, mm_into, nt_into, nt_mm
 from .gemm_tn import gemm_tn_, supported as _tn_supported
 from .transpose import transpose
 

@@ -17,8 +17,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from ._grad import deliver, mm_into
-from .gemm_nt import nt_into, nt_mm
+from ._grad import deliver, mm_into, nt_into, nt_mm
 from .linear import _DGRAD_NT, linear
 from .swiglu import swiglu, swiglu_reference
 from .transpose import transpose
