@@ -15,7 +15,7 @@ from tensorhive_fixed_amd.ops.gemm_tn import default_splitk, gemm_tn_  # noqa: E
 
 T = 32768
 SHAPES = [("wqkv", 6144, 4096), ("wo", 4096, 4096), ("w2", 4096, 14336), ("w13", 28672, 4096)]
-MODES = [int(x) for x in os.environ.get("TN_MODES", "6,9").split(",")]
+MODES = [int(x) for x in os.environ.get("TN_MODES", "6,9,10").split(",")]
 
 
 def timed(fn, iters=10):
@@ -34,7 +34,7 @@ def main():
     _lib.load()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    for (K, M, N) in ((64, 256, 256), (128, 512, 256), (4096, 256, 768), (2048, 768, 512)):
+    for (K, M, N) in ((64, 256, 256), (128, 512, 256), (4096, 256, 768), (2048, 768, 512), (256, 4096, 4352)):
         a = torch.randn(K, M, device=dev, dtype=torch.bfloat16, generator=g)
         b = torch.randn(K, N, device=dev, dtype=torch.bfloat16, generator=g)
         ref = a.float().t() @ b.float()

@@ -760,14 +760,14 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_tn_w4_kernel(
 template <bool SPLIT, bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
-    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk) {
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int tile0) {
   constexpr int HIMG = 64 * ROWB;     // 32 KB: 64 k-rows x 256 columns
   constexpr int HSTAGE = 2 * HIMG;    // A | B
   __shared__ __attribute__((aligned(1024))) char smem_raw[2 * HSTAGE];
   const char LDS_AS* smem = (const char LDS_AS*)smem_raw;
   const int nM = M / TM, nN = N / TN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = SPLIT ? L / splitk : L;
+  const int tile = tile0 + (SPLIT ? L / splitk : L);
   const int split = SPLIT ? L % splitk : 0;
   constexpr int GM = TH_TN_GM;
   const int per_band = GM * nN;
@@ -983,6 +983,37 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *cp = o;
 }
 
+// Split-K remainder of the "data-parallel + split" launch: C tile (+)= sum over splits of its slab
+// tiles, for the tiles [tile0, tile0 + gridDim.x) of the band order; one workgroup per tile.
+__global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
+                                                                  long ldc, int M, int N, int splitk, int beta, int tile0) {
+  const int nM = M / TM, nN = N / TN;
+  const int tile = tile0 + blockIdx.x;
+  constexpr int GM = TH_TN_GM;
+  const int per_band = GM * nN;
+  const int band = tile / per_band, first_m = band * GM, gm = min(GM, nM - first_m);
+  const int in_band = tile % per_band;
+  const long m0 = (long)(first_m + in_band % gm) * TM, n0 = (long)(in_band / gm) * TN;
+  for (int e = threadIdx.x * 8; e < TM * TN; e += 256 * 8) {
+    const long m = m0 + e / TN, n = n0 + e % TN;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    for (int sp = 0; sp < splitk; ++sp) {
+      const float4v* p = reinterpret_cast<const float4v*>(slab + ((long)sp * M + m) * N + n);
+      const float4v x0 = p[0], x1 = p[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += x0[j]; v[4 + j] += x1[j]; }
+    }
+    ushort8* cp = reinterpret_cast<ushort8*>(C + m * ldc + n);
+    ushort8 o;
+    const ushort8 c = beta ? *cp : ushort8(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] + (beta ? bf2f(c[j]) : 0.f));
+    *cp = o;
+  }
+}
+
 // C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  splitk > 1 needs a
 // workspace of splitk*M*N floats.  Returns -1 for shapes the kernel does not tile.
 // flags: bit0 = ping-pong schedule (gemm_tn_pp_kernel) instead of the lockstep 2-barrier loop;
@@ -991,7 +1022,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 //        bit3 = one wave per SIMD, 128 x 128 per wave (gemm_tn_w4_kernel, 256 threads);
 //        bit4 (with bit1) = v_mfma_f32_16x16x32_bf16 fragments in the ping-pong v2 kernel;
 //        bit5 (with bit1) = row swizzle S(r) = (r + (r >> 3)) & 3 of the v2 images;
-//        bit6 = schedule "hb" (gemm_tn_hb_kernel: one wave per SIMD, 16x16x32 asm MFMAs, per-operand barriers)
+//        bit6 = schedule "hb" (gemm_tn_hb_kernel: one wave per SIMD, 16x16x32 asm MFMAs, per-operand barriers);
+//        bit7 (with bit6, splitk > 1) = data-parallel whole tiles + split-K only for the remainder tiles
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -1028,9 +1060,25 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
     if (K / splitk < 64 || (K / splitk) % 64) return -1;
     // buffer descriptors per k-tile: 32-bit offsets over 64 k-rows of one operand
     if (2L * 64 * max(lda, ldb) + 512 >= (1L << 31)) return -1;
-    if (splitk > 1) gemm_tn_hb_kernel<true, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk);
-    else if (beta) gemm_tn_hb_kernel<false, true><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1);
-    else gemm_tn_hb_kernel<false, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1);
+    // flags bit7 with splitk > 1: data-parallel rounds of whole tiles on every CU (direct bf16 output),
+    // then only the REMAINDER tiles split `splitk` ways (slab + a per-tile reduce): no split-K slab
+    // round trip for the bulk of the tiles and no half-empty last round
+    const long cus = 256;
+    const long full = (flags & 128) && splitk > 1 ? tiles / cus * cus : 0;
+    const long rem = tiles - full;
+    if (full > 0 && rem * splitk <= cus) {
+      if (beta) gemm_tn_hb_kernel<false, true><<<(unsigned)full, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
+      else gemm_tn_hb_kernel<false, false><<<(unsigned)full, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
+      if (rem > 0) {
+        gemm_tn_hb_kernel<true, false><<<(unsigned)(rem * splitk), 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K,
+                                                                                splitk, (int)full);
+        splitk_reduce_tiles_kernel<<<(unsigned)rem, 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta, (int)full);
+      }
+      TH_CHECK_LAUNCH();
+    }
+    if (splitk > 1) gemm_tn_hb_kernel<true, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, 0);
+    else if (beta) gemm_tn_hb_kernel<false, true><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
+    else gemm_tn_hb_kernel<false, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
   } else if (flags & 8) {
     if (splitk > 1) gemm_tn_w4_kernel<true><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta);
     else gemm_tn_w4_kernel<false><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);

@@ -42,8 +42,9 @@ def default_splitk(m: int, n: int, k: int, cus: int = 256) -> int:
 # (4-stage ring of 32-deep k-tiles, per-group DMA 2 k-tiles ahead), 3 = v2 with the DMA 3 ahead,
 # 4 = one wave per SIMD with 128 x 128 per wave, 5 = v2 with v_mfma_f32_16x16x32_bf16 fragments,
 # 6 / 7 / 8 = modes 2 / 5 / 3 with the (r + r>>3) row swizzle, 9 = "hb": one wave per SIMD with 16x16x32
-# asm MFMAs (AGPR accumulators), 64-deep k-tiles, per-operand barriers (gemm_tn_hb_kernel)
-_PP = int(os.environ.get("TH_GEMM_TN_PP", "9"))  # hb: +1.2 % step, profiles/r05_gemm
+# asm MFMAs (AGPR accumulators), 64-deep k-tiles, per-operand barriers (gemm_tn_hb_kernel), 10 = hb with
+# whole tiles data-parallel and only the remainder tiles split-K
+_PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))  # hb + data-parallel/remainder split: profiles/r05_gemm
 
 
 def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
@@ -69,5 +70,5 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
     ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
               M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
-              {0: 0, 1: 1, 2: 2, 3: 6, 4: 8, 5: 18, 6: 34, 7: 50, 8: 38, 9: 64}[int(_PP if pingpong is None else pingpong)], _lib.stream_ptr(a.device))
+              {0: 0, 1: 1, 2: 2, 3: 6, 4: 8, 5: 18, 6: 34, 7: 50, 8: 38, 9: 64, 10: 192}[int(_PP if pingpong is None else pingpong)], _lib.stream_ptr(a.device))
     return out
