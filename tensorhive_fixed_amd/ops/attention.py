@@ -77,8 +77,7 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
 
     ``variant`` (0-31, experiments only) selects a kernel variant: bit0 Q pre-scaling, bit1
     deferred rescale, bit2 double-buffered K/V tiles, bit3 KV-major block order, bit4 (with all of
-    0-3) the tile DMA spread over the S chain, bit5 the one-wave-per-SIMD kernel (``fa_fwd_w1_kernel``,
-    S % 256 == 0); ``None`` = the built-in default."""
+    0-3) the tile DMA spread over the S chain; ``None`` = the built-in default."""
     row = qkv.shape[1]
     if qkv.dtype != torch.bfloat16 or not qkv.is_contiguous() or Dh != 128:
         raise ValueError("flash kernel needs contiguous bf16 packed qkv and head_dim 128")
@@ -91,8 +90,7 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
     v = k + Hkv * Dh * 2
     _lib.call("th_flash_attn_fwd", q, k, v, o.data_ptr(), lse.data_ptr(), B, S, Hq, Hkv, Dh,
               int(causal), row, S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh),
-              0 if variant is None else (16 + (int(variant) & 15) + 32 * ((int(variant) >> 4) & 1)
-                                         + 64 * ((int(variant) >> 5) & 1)),
+              0 if variant is None else 16 + (int(variant) & 15) + 32 * ((int(variant) >> 4) & 1),
               _lib.stream_ptr(qkv.device))
     return o, lse
 

@@ -1584,277 +1584,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kf_kernel(
   }
 }
 
-// ---------------------------------------------- forward, one wave per SIMD, 64 queries per wave (w1)
-// The cdna_hip_programming.md attention-forward structure on this file's operand orientation:
-//   * workgroup = 4 waves = 256 queries of one (batch, q head); wave = 64 queries as two 32-query
-//     blocks x = 0, 1; one wave per SIMD, so the O^T accumulators of both blocks (2 x 4 f32x16 = 128)
-//     live in the AGPRs, pinned by inline-asm MFMAs, and the S^T chains / softmax in the arch VGPRs;
-//   * 64-key tiles by LDS-DMA into a 4-deep ring (128 KB): tile j+2 is issued after the barrier of
-//     tile j, whose wait is the counted vmcnt(8) (tile j+1 stays in flight); one barrier per tile;
-//   * per tile four phases of 16 MFMAs, the softmax of one block always in the gaps of the other's
-//     MFMAs (one exponential per gap, the guide's filler budget):
-//         A: S^T(x0, j)    || exps of keys 32-63 of (x1, j-1), P pack, row sums; this wave's 8 DMA pieces
-//         B: O^T(x1) += V(j-1)^T P(x1, j-1)   || after a short head (mask, row max, rescale vote):
-//                                                exps of keys 0-31 of (x0, j)
-//         C: S^T(x1, j)    || exps of keys 32-63 of (x0, j)
-//         D: O^T(x0) += V(j)^T P(x0, j)       || head + exps of keys 0-31 of (x1, j)
-//     so P(x1) runs one tile behind; a wave drains its last tile and then only joins the remaining
-//     tiles' barriers and DMA (causal: its diagonal is its last tile);
-//   * the rare rescale (running max grew by > F_DEFER_THR) multiplies that block's O in a
-//     wave-uniform branch between phases, when no MFMA writes it.
-// S % 256 == 0 (the launcher falls back to fa_fwd_kernel otherwise).
-constexpr int W1_BM = 256, W1_BN = 64, W1_TILEB = 2 * W1_BN * 256;  // K | V images of one tile, 32 KB
-
-__device__ __forceinline__ void w1_dma_piece(const ushort* Kb, const ushort* Vb, long ld, int S, int src, int buf,
-                                             unsigned lds0, int wu, const unsigned (&rc)[4], int p) {
-  const unsigned img = lds0 + (buf & 3) * W1_TILEB + wu * 4096;
-  const int u = p >> 1;
-  const int row = min(src * W1_BN + (int)(rc[u] & 255), S - 1);
-  const unsigned voff = (unsigned)(row * ld + (rc[u] >> 8) * 8) * 2u;
-  if (p & 1)
-    glds16(Vb, voff, img + W1_BN * 256 + u * 1024);
-  else
-    glds16(Kb, voff, img + u * 1024);
-}
-
-__global__ __launch_bounds__(256, 1) void fa_fwd_w1_kernel(
-    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
-    ushort* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hkv, long ld,
-    long bs, long ldo, long bso, float scale_log2, int causal) {
-  __shared__ __attribute__((aligned(1024))) char smem[4 * W1_TILEB];
-  const int nqb = S / W1_BM;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  int b, hq, qb;
-  q_block_map<true>(L, nqb, B, Hq, Hkv, b, hq, qb);
-  const int hk = hq / (Hq / Hkv);
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c32 = lane & 31;
-  const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q0 = qb * W1_BM + wu * 64;
-  const ushort* Qb = Q + b * bs + (long)hq * HD;
-  const ushort* Kb = K + b * bs + (long)hk * HD;
-  const ushort* Vb = V + b * bs + (long)hk * HD;
-
-  bf16x8 qf[2][8];  // Q prescaled by softmax_scale * log2(e)
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      ushort8 u = *reinterpret_cast<const ushort8*>(Qb + (long)(q0 + 32 * x + c32) * ld + 16 * s + 8 * h);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
-      qf[x][s] = as_bf(u);
-    }
-  const int ntiles = causal ? (qb + 1) * (W1_BM / W1_BN) : S / W1_BN;  // the workgroup's key tiles
-  const int last = causal ? (q0 + 63) / W1_BN : ntiles - 1;              // this wave's last (diagonal) tile
-  unsigned rc[4];
-  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q loads retired by a wait the compiler sees
-#pragma unroll
-  for (int u = 0; u < 4; ++u) rc[u] = img_rc(wu * 4096 + u * 1024 + lane * 16);
-  // prologue: tile 0 into buffers 0 AND 3 (buffer 3 = "tile -1", read by the first PV(x1) with P = 0),
-  // tile 1 into buffer 1
-#pragma unroll
-  for (int p = 0; p < 8; ++p) w1_dma_piece(Kb, Vb, ld, S, 0, 0, lds0, wu, rc, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) w1_dma_piece(Kb, Vb, ld, S, 0, 3, lds0, wu, rc, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) w1_dma_piece(Kb, Vb, ld, S, min(1, ntiles - 1), 1, lds0, wu, rc, p);
-
-  f32x16 o[2][4];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[x][d] = f32x16(0.f);
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) asm volatile("" : "+a"(o[x][d]));
-  asm volatile("s_nop 4" ::);
-
-  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f}, m_base[2] = {0.f, 0.f};
-  f32x16 sacc[2][2];
-  bf16x8 pf[2][4];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    sacc[1][kb] = f32x16(-INFINITY);  // "tile -1" of block 1: P = 0
-    sacc[0][kb] = f32x16(0.f);
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    pf[0][k] = as_bf(ushort8(0));
-    pf[1][k] = as_bf(ushort8(0));
-  }
-  float rs4[4] = {0.f, 0.f, 0.f, 0.f};
-
-  // S^T chain operand i (0-15) of a phase: K row block i & 1, k-step i >> 1
-  auto kop = [&](const char* ks, int i) { return lds_row(ks, 32 * (i & 1) + c32, 2 * (i >> 1) + h); };
-  // PV operand i: V^T rows (keys) 16 (i >> 2) .., dims 32 (i & 3) ..
-  auto vop = [&](const char* vs, int i) { return lds_tr(vs, 16 * (i >> 2), 32 * (i & 3), lane); };
-  auto exp_el = [&](int x, int kb, int r) {
-    const float pv = fast_exp2(sacc[x][kb][r]);
-    sacc[x][kb][r] = pv;
-    rs4[r & 3] += pv;
-  };
-  auto finish_rows = [&](int x) {
-    const float rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
-    l_i[x] += half_swap_sum(rs);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) rs4[e] = 0.f;
-  };
-  // head of block x's softmax on tile j: mask (its diagonal tile), row max, the rescale vote and the
-  // rare rescale of O[x] / l / the scores (no MFMA writes O[x] here)
-  auto head = [&](int x, int j) {
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(sacc[x][0]), "+v"(sacc[x][1]));
-    if (causal && j == last) {  // key 32 kb + row > query 32 x + c32 of this 64-key tile
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (32 * kb + acc_row(r, h) > 32 * x + c32) sacc[x][kb][r] = -INFINITY;
-    }
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, sacc[x][kb][r]);
-    mt = half_swap_max(mt);
-    if (!__all(mt + m_base[x] - m_i[x] <= F_DEFER_THR)) {
-      const float m_new = fmaxf(m_i[x], mt + m_base[x]);
-      const float mu = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = fast_exp2(m_i[x] - mu);
-      l_i[x] *= alpha;
-      if (j > 0) {  // O is still zero before the first tile
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          o[x][d] *= alpha;
-          asm volatile("" : "+a"(o[x][d]));
-        }
-      }
-      m_i[x] = m_new;
-      const float shift = mu - m_base[x];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) sacc[x][kb] -= shift;
-      m_base[x] = mu;
-    }
-  };
-  auto pack_half = [&](int x, int kb) {
-    pf[x][2 * kb] = pack8(sacc[x][kb], 0);
-    pf[x][2 * kb + 1] = pack8(sacc[x][kb], 8);
-  };
-
-  asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // tile 0 (buffers 0 and 3) landed
-  for (int j = 0; j <= last; ++j) {
-    if (j > 0) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // tile j landed
-    const char* ks = smem + (j & 3) * W1_TILEB;
-    const char* vs_prev = smem + ((j + 3) & 3) * W1_TILEB + W1_BN * 256;
-    const char* vs = ks + W1_BN * 256;
-    const int src2 = min(j + 2, ntiles - 1);  // past the end: re-stage the last tile (nobody reads it)
-    // ---- phase A: S^T(x0, j) || keys 32-63 of (x1, j-1) + DMA of tile j+2
-    {
-      sacc[0][0] = f32x16(-m_base[0]);
-      sacc[0][1] = f32x16(-m_base[0]);
-      bf16x8 op[3];
-      op[0] = kop(ks, 0);
-      op[1] = kop(ks, 1);
-      static_for<0, 16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i + 2 < 16) op[(i + 2) % 3] = kop(ks, i + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_v<(i < 2)>(sacc[0][i & 1], op[i % 3], qf[0][i >> 1]);
-        exp_el(1, 1, i);
-        if constexpr (i & 1) w1_dma_piece(Kb, Vb, ld, S, src2, j + 2, lds0, wu, rc, i >> 1);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      pack_half(1, 1);
-      finish_rows(1);
-    }
-    // ---- phase B: O^T(x1) += V(j-1)^T P(x1, j-1) || head + keys 0-31 of (x0, j)
-    head(0, j);
-    {
-      bf16x8 op[3];
-      op[0] = vop(vs_prev, 0);
-      op[1] = vop(vs_prev, 1);
-      static_for<0, 16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i + 2 < 16) op[(i + 2) % 3] = vop(vs_prev, i + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_a<(i % 4 == 0)>(o[1][i & 3], op[i % 3], pf[1][i >> 2]);
-        exp_el(0, 0, i);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      pack_half(0, 0);
-    }
-    // ---- phase C: S^T(x1, j) || keys 32-63 of (x0, j)
-    {
-      sacc[1][0] = f32x16(-m_base[1]);
-      sacc[1][1] = f32x16(-m_base[1]);
-      bf16x8 op[3];
-      op[0] = kop(ks, 0);
-      op[1] = kop(ks, 1);
-      static_for<0, 16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i + 2 < 16) op[(i + 2) % 3] = kop(ks, i + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_v<(i < 2)>(sacc[1][i & 1], op[i % 3], qf[1][i >> 1]);
-        exp_el(0, 1, i);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      pack_half(0, 1);
-      finish_rows(0);
-    }
-    // ---- phase D: O^T(x0) += V(j)^T P(x0, j) || head + keys 0-31 of (x1, j)
-    head(1, j);
-    {
-      bf16x8 op[3];
-      op[0] = vop(vs, 0);
-      op[1] = vop(vs, 1);
-      static_for<0, 16>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i + 2 < 16) op[(i + 2) % 3] = vop(vs, i + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_a<(i % 4 == 0)>(o[0][i & 3], op[i % 3], pf[0][i >> 2]);
-        exp_el(1, 0, i);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      pack_half(1, 0);
-    }
-  }
-  // drain: keys 32-63 of (x1, last), then its PV
-#pragma unroll
-  for (int r = 0; r < 16; ++r) exp_el(1, 1, r);
-  pack_half(1, 1);
-  finish_rows(1);
-  {
-    const char* vl = smem + (last & 3) * W1_TILEB + W1_BN * 256;
-    static_for<0, 16>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      const bf16x8 vt = vop(vl, i);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_a<(i % 4 == 0)>(o[1][i & 3], vt, pf[1][i >> 2]);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-  // the workgroup's remaining tiles: only this wave's barrier and DMA share
-  for (int j = last + 1; j < ntiles; ++j) {
-    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-    const int src2 = min(j + 2, ntiles - 1);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) w1_dma_piece(Kb, Vb, ld, S, src2, j + 2, lds0, wu, rc, p);
-  }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) asm volatile("" : "+a"(o[x][d]));
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    const int q = q0 + 32 * x + c32;
-    const float inv_l = l_i[x] > 0.f ? 1.f / l_i[x] : 0.f;
-    store_row_t21(O + b * bso + (long)q * ldo + (long)hq * HD, o[x], inv_l, h);
-    if (h == 0) LSE[((long)b * Hq + hq) * S + q] = (m_i[x] + log2f(l_i[x])) * LN2;
-  }
-}
-
 constexpr int B_LDS = 2 * B_BK * 256 + 2 * B_BQ * 256 + 2 * B_BQ * 4;
 }  // namespace
 
@@ -1868,14 +1597,6 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
                                  int B, int S, int Hq, int Hkv, int D, int causal, long ld, long bs,
                                  long ldo, long bso, float scale, int flags, hipStream_t s) {
   if (check_geom(B, S, Hq, Hkv, D, ld, ldo)) return -1;
-  // flags bit6: the one-wave-per-SIMD forward (fa_fwd_w1_kernel; S % 256 == 0, 32-bit DMA offsets)
-  if ((flags & 64) && S % W1_BM == 0 && (long)S * ld * 2 < (1L << 31)) {
-    const long nw1 = (long)(S / W1_BM) * Hq * B;
-    fa_fwd_w1_kernel<<<(unsigned)nw1, 256, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v, (ushort*)o,
-                                                    lse, B, S, Hq, Hkv, ld, bs, ldo, bso, scale * LOG2E, causal);
-    TH_CHECK_LAUNCH();
-  }
-  flags &= ~64;
   const long nblk = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags: 0 = default variant; 16 + v = explicit v (bit0 PRESCALE, bit1 DEFER, bit2 DBUF,
   // bit3 KVMAJOR block order)
