@@ -760,7 +760,8 @@ __global__ __launch_bounds__(W4_THR, 1) void gemm_tn_w4_kernel(
 template <bool SPLIT, bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
-    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int tile0) {
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int tile0,
+    int GM) {
   constexpr int HIMG = 64 * ROWB;     // 32 KB: 64 k-rows x 256 columns
   constexpr int HSTAGE = 2 * HIMG;    // A | B
   __shared__ __attribute__((aligned(1024))) char smem_raw[2 * HSTAGE];
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = tile0 + (SPLIT ? L / splitk : L);
   const int split = SPLIT ? L % splitk : 0;
-  constexpr int GM = TH_TN_GM;
+  // GM: output-tile rows per XCD band (runtime: launch flags bits 8-11, default TH_TN_GM)
   const int per_band = GM * nN;
   const int band = tile / per_band;
   const int first_m = band * GM;
@@ -986,10 +987,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // Split-K remainder of the "data-parallel + split" launch: C tile (+)= sum over splits of its slab
 // tiles, for the tiles [tile0, tile0 + gridDim.x) of the band order; one workgroup per tile.
 __global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
-                                                                  long ldc, int M, int N, int splitk, int beta, int tile0) {
+                                                                  long ldc, int M, int N, int splitk, int beta, int tile0,
+                                                                  int GM) {
   const int nM = M / TM, nN = N / TN;
   const int tile = tile0 + blockIdx.x;
-  constexpr int GM = TH_TN_GM;
   const int per_band = GM * nN;
   const int band = tile / per_band, first_m = band * GM, gm = min(GM, nM - first_m);
   const int in_band = tile % per_band;
@@ -1023,7 +1024,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* _
 //        bit4 (with bit1) = v_mfma_f32_16x16x32_bf16 fragments in the ping-pong v2 kernel;
 //        bit5 (with bit1) = row swizzle S(r) = (r + (r >> 3)) & 3 of the v2 images;
 //        bit6 = schedule "hb" (gemm_tn_hb_kernel: one wave per SIMD, 16x16x32 asm MFMAs, per-operand barriers);
-//        bit7 (with bit6, splitk > 1) = data-parallel whole tiles + split-K only for the remainder tiles
+//        bit7 (with bit6, splitk > 1) = data-parallel whole tiles + split-K only for the remainder tiles;
+//        bits 8-11 (with bit6) = XCD band height in tile rows (0 = TH_TN_GM)
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
                           int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || K % (TK * splitk)) return -1;
@@ -1057,6 +1059,7 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
     else KERNEL<false, AH><<<grid, NTHR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);             \
   } while (0)
   if (flags & 64) {  // schedule "hb": one wave per SIMD, 64-deep k-tiles
+    const int gmr = ((flags >> 8) & 15) ? ((flags >> 8) & 15) : TH_TN_GM;  // XCD band height (tile rows)
     if (K / splitk < 64 || (K / splitk) % 64) return -1;
     // buffer descriptors per k-tile: 32-bit offsets over 64 k-rows of one operand
     if (2L * 64 * max(lda, ldb) + 512 >= (1L << 31)) return -1;
@@ -1067,18 +1070,18 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
     const long full = (flags & 128) && splitk > 1 ? tiles / cus * cus : 0;
     const long rem = tiles - full;
     if (full > 0 && rem * splitk <= cus) {
-      if (beta) gemm_tn_hb_kernel<false, true><<<(unsigned)full, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
-      else gemm_tn_hb_kernel<false, false><<<(unsigned)full, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
+      if (beta) gemm_tn_hb_kernel<false, true><<<(unsigned)full, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0, gmr);
+      else gemm_tn_hb_kernel<false, false><<<(unsigned)full, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0, gmr);
       if (rem > 0) {
         gemm_tn_hb_kernel<true, false><<<(unsigned)(rem * splitk), 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K,
-                                                                                splitk, (int)full);
-        splitk_reduce_tiles_kernel<<<(unsigned)rem, 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta, (int)full);
+                                                                                splitk, (int)full, gmr);
+        splitk_reduce_tiles_kernel<<<(unsigned)rem, 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta, (int)full, gmr);
       }
       TH_CHECK_LAUNCH();
     }
-    if (splitk > 1) gemm_tn_hb_kernel<true, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, 0);
-    else if (beta) gemm_tn_hb_kernel<false, true><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
-    else gemm_tn_hb_kernel<false, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0);
+    if (splitk > 1) gemm_tn_hb_kernel<true, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, 0, gmr);
+    else if (beta) gemm_tn_hb_kernel<false, true><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0, gmr);
+    else gemm_tn_hb_kernel<false, false><<<grid, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, 0, gmr);
   } else if (flags & 8) {
     if (splitk > 1) gemm_tn_w4_kernel<true><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, splitk, beta);
     else gemm_tn_w4_kernel<false><<<grid, W4_THR, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, beta);
