@@ -43,17 +43,19 @@ def test_gemm_tn_strided_operands_and_asymmetry(pingpong):
     assert (out.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-2
 
 
+@pytest.mark.parametrize("band", [0, 1, 16])
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_gemm_tn_data_parallel_plus_remainder_split(accumulate):
+def test_gemm_tn_data_parallel_plus_remainder_split(accumulate, band):
     """Mode 10: 272 tiles = one data-parallel round of 256 whole tiles + 16 remainder tiles split 2 ways
-    (slab + per-tile reduce); every tile of both parts must match fp32."""
+    (slab + per-tile reduce); every tile of both parts must match fp32, for several XCD band heights
+    (the remainder tiles and the reduce kernel follow the same band map)."""
     K, M, N = 256, 4096, 4352
     g = torch.Generator(device="cuda").manual_seed(5)
     a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16, generator=g)
     b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16, generator=g)
     out = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g)
     ref = a.float().t() @ b.float() + (out.float() if accumulate else 0)
-    gemm_tn_(a, b, out, accumulate=accumulate, splitk=2, pingpong=10)
+    gemm_tn_(a, b, out, accumulate=accumulate, splitk=2, pingpong=10, band=band)
     torch.cuda.synchronize()
     err = (out.float() - ref).abs().max().item()
     assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
