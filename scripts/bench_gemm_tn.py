@@ -35,7 +35,7 @@ def main():
         o1 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         o2 = torch.empty_like(o1)
         variants = {"hipblaslt": lambda: torch.mm(a.t(), b, out=o1)}
-        pps = [int(x) for x in os.environ.get("TN_PP", "1,2,4").split(",")]
+        pps = [int(x) for x in os.environ.get("TN_PP", "9,10").split(",")]
         sks = sorted({1, 2, default_splitk(M, N, T)}) if os.environ.get("TN_ALL_SPLITK", "1") == "1" \
             else [default_splitk(M, N, T)]
         for sk in sks:

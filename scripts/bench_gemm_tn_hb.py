@@ -15,7 +15,7 @@ from tensorhive_fixed_amd.ops.gemm_tn import default_splitk, gemm_tn_  # noqa: E
 
 T = 32768
 SHAPES = [("wqkv", 6144, 4096), ("wo", 4096, 4096), ("w2", 4096, 14336), ("w13", 28672, 4096)]
-MODES = [int(x) for x in os.environ.get("TN_MODES", "6,9,10").split(",")]
+MODES = [int(x) for x in os.environ.get("TN_MODES", "9,10").split(",")]
 
 
 def timed(fn, iters=10):

@@ -15,7 +15,7 @@ M, N, K = 4096, 4096, 32768
 a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
 b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
 o = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-for pp in [int(x) for x in os.environ.get("TN_SCHEDULES", "2").split(",")]:
+for pp in [int(x) for x in os.environ.get("TN_SCHEDULES", "9").split(",")]:
     for _ in range(5):
         gemm_tn_(a, b, o, splitk=1, pingpong=pp)
 aT, bT = a.t().contiguous(), b.t().contiguous()  # [M, K], [N, K]: K-contiguous operands

@@ -38,12 +38,10 @@ def default_splitk(m: int, n: int, k: int, cus: int = 256) -> int:
     return best
 
 
-# schedule: 0 = lockstep 2-barrier loop, 1 = ping-pong (2-stage, 64-deep k-tiles), 2 = ping-pong v2
-# (4-stage ring of 32-deep k-tiles, per-group DMA 2 k-tiles ahead), 3 = v2 with the DMA 3 ahead,
-# 4 = one wave per SIMD with 128 x 128 per wave, 5 = v2 with v_mfma_f32_16x16x32_bf16 fragments,
-# 6 / 7 / 8 = modes 2 / 5 / 3 with the (r + r>>3) row swizzle, 9 = "hb": one wave per SIMD with 16x16x32
-# asm MFMAs (AGPR accumulators), 64-deep k-tiles, per-operand barriers (gemm_tn_hb_kernel), 10 = hb with
-# whole tiles data-parallel and only the remainder tiles split-K
+# launch mode of the hb kernel (csrc/gemm_tn.hip, the only schedule since round 5; the round-1..4 modes 0-8
+# were retired, profiles/r05_gemm/): 9 = whole-K tiles, or split-K for every tile when splitk > 1;
+# 10 = whole tiles data-parallel on every CU, split-K only for the remainder tiles
+_MODES = {9: 64, 10: 192}
 _PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))  # hb + data-parallel/remainder split: profiles/r05_gemm
 
 
@@ -59,6 +57,9 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
         r = a.float().t() @ b.float()
         out.copy_((out.float() + r if accumulate else r).to(out.dtype))
         return out
+    mode = int(_PP if pingpong is None else pingpong)
+    if mode not in _MODES:
+        raise ValueError(f"gemm_tn_: launch mode {mode} not in {sorted(_MODES)}")
     sk = default_splitk(M, N, K) if splitk is None else splitk
     ok = (a.dtype == b.dtype == out.dtype == torch.bfloat16 and supported(M, N, K, sk)
           and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1)
@@ -71,6 +72,5 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
     ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
               M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
-              {0: 0, 1: 1, 2: 2, 3: 6, 4: 8, 5: 18, 6: 34, 7: 50, 8: 38, 9: 64, 10: 192}[int(_PP if pingpong is None else pingpong)]
-              | ((int(band) & 15) << 8), _lib.stream_ptr(a.device))
+              _MODES[mode] | ((int(band) & 15) << 8), _lib.stream_ptr(a.device))
     return out

@@ -16,7 +16,7 @@ def _load():
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 64, 1), (512, 768, 1024, 1), (768, 512, 4096, 2),
                                           (1024, 256, 2048, 4), (256, 1280, 640, 1)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("pingpong", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("pingpong", [9, 10])
 def test_gemm_tn_matches_fp32(M, N, K, splitk, accumulate, pingpong):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
     a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16, generator=g)
@@ -29,7 +29,7 @@ def test_gemm_tn_matches_fp32(M, N, K, splitk, accumulate, pingpong):
     assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
 
 
-@pytest.mark.parametrize("pingpong", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("pingpong", [9, 10])
 def test_gemm_tn_strided_operands_and_asymmetry(pingpong):
     """Row-strided views (a slice of a wider activation) and an asymmetric operand pair catch a
     swapped row/column map."""
