@@ -46,20 +46,21 @@ _PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))  # hb + data-parallel/remainder
 
 
 def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-             splitk: int | None = None, pingpong: int | None = None, band: int = 0) -> torch.Tensor:
+             splitk: int | None = None, pingpong: int | None = None, band: int = 0,
+             pv: int = 0) -> torch.Tensor:
     """``out[M, N] (+)= a[K, M]ᵀ @ b[K, N]`` (bf16 in / out, f32 accumulation).  ``band``: XCD band
     height in output-tile rows for the hb modes (0 = the compiled default)."""
     K, M = a.shape
     K2, N = b.shape
     if K2 != K or tuple(out.shape) != (M, N):
         raise ValueError(f"gemm_tn_: shapes {tuple(a.shape)}, {tuple(b.shape)} -> {tuple(out.shape)}")
+    mode = int(_PP if pingpong is None else pingpong)
+    if mode not in _MODES:
+        raise ValueError(f"gemm_tn_: launch mode {mode} not in {sorted(_MODES)}")
     if not a.is_cuda:
         r = a.float().t() @ b.float()
         out.copy_((out.float() + r if accumulate else r).to(out.dtype))
         return out
-    mode = int(_PP if pingpong is None else pingpong)
-    if mode not in _MODES:
-        raise ValueError(f"gemm_tn_: launch mode {mode} not in {sorted(_MODES)}")
     sk = default_splitk(M, N, K) if splitk is None else splitk
     ok = (a.dtype == b.dtype == out.dtype == torch.bfloat16 and supported(M, N, K, sk)
           and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1)
@@ -72,5 +73,5 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
     ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
               M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
-              _MODES[mode] | ((int(band) & 15) << 8), _lib.stream_ptr(a.device))
+              _MODES[mode] | ((int(band) & 15) << 8) | ((int(pv) & 7) << 13), _lib.stream_ptr(a.device))
     return out

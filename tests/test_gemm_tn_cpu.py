@@ -42,3 +42,12 @@ def test_mismatched_shapes_are_rejected():
     b = torch.zeros(32, 40, dtype=torch.bfloat16)
     with pytest.raises(ValueError):
         gemm_tn_(a, b, torch.zeros(24, 40, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("mode", [0, 6, 8, 11])
+def test_retired_launch_modes_are_rejected(mode):
+    """Only the hb schedule's launch modes 9 / 10 exist since round 5 (profiles/r05_gemm/)."""
+    a = torch.zeros(64, 24, dtype=torch.bfloat16)
+    b = torch.zeros(64, 40, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        gemm_tn_(a, b, torch.zeros(24, 40, dtype=torch.bfloat16), pingpong=mode)
