@@ -145,12 +145,17 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
                uint64_t) {},
             nullptr, &a->buf) != ROCPROFILER_STATUS_SUCCESS)
       continue;
-    configure(a);
-    if (a->config.handle == 0) continue;
+    // The counter config is NOT built here: enumerating the agent's counters (configure()) takes
+    // seconds, and tool_init runs inside the task's HSA initialisation (its `import torch`), so every
+    // task would start that much later (profiles/r05_daemon/startup.txt).  The service only needs the
+    // config when a context starts; the sampler thread builds it first.
     if (rocprofiler_configure_device_counting_service(
             a->ctx, a->buf, info.id,
             [](rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_device_counting_agent_cb_t set,
-               void* ud) { set(ctx, static_cast<Agent*>(ud)->config); },
+               void* ud) {
+              auto* ag = static_cast<Agent*>(ud);
+              if (ag->config.handle != 0) set(ctx, ag->config);
+            },
             a) != ROCPROFILER_STATUS_SUCCESS)
       continue;
     g_agents.push_back(a);
@@ -181,9 +186,16 @@ void sampler() {
   const char* o = getenv("TH_HBM_OUT");
   const std::string path = o && *o ? o : "/dev/shm/th-hbm-" + std::to_string((long)getpid()) + ".json";
   const bool append = getenv("TH_HBM_APPEND") && !strcmp(getenv("TH_HBM_APPEND"), "1");
-  // let the runtime finish initialising before the first context start
+  // let the runtime finish initialising, then build the counter configs (off the task's startup path)
   for (int i = 0; i < 10 && !g_stop; ++i) usleep(50000);
-  while (!g_stop) {
+  std::vector<Agent*> live;
+  for (auto* a : g_agents) {
+    if (g_stop) return;
+    configure(a);
+    if (a->config.handle != 0) live.push_back(a);
+  }
+  g_agents.swap(live);
+  while (!g_stop && !g_agents.empty()) {
     for (auto* a : g_agents) rocprofiler_start_context(a->ctx);
     const uint64_t t0 = now_ns();
     for (int slept = 0; slept < period_ms && !g_stop; slept += 10) usleep(10000);

@@ -67,7 +67,7 @@ __device__ __forceinline__ void static_for_tn(F&& f) {
 //              | 44 barrier;  52- 87 DMA B of tile t+2 (8 pieces, every 5th MFMA)
 //       MFMA  64-127  k-step 1 (Y); 88: vmcnt(16) + barrier (tile t+1 landed); 90-121 read X of tile t+1
 //   * epilogue: bf16 through LDS with 16-B row stores (beta: C added), or f32x4 stores into the split-K slab.
-template <bool SPLIT, bool BETA, int WV = 0>
+template <bool SPLIT, bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
     ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int tile0,
@@ -205,24 +205,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       }
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece(1, (m - b0) / bs, kt2, st);
-      if constexpr (WV == 1) {
-        // two-phase wait: tile t+1's A pieces (the oldest 8 in flight) at 88, its B pieces at 105
-        if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
-        if constexpr (m == 105) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-        if constexpr (m >= 89 && m <= 104) {
-          constexpr int h = m - 89, f = h >> 1;
-          if constexpr (!(h & 1)) lo_x = rd_half(s_nxt, f, 0, 0);
-          else xa[f] = join(lo_x, rd_half(s_nxt, f, 0, 1));
-        }
-        if constexpr (m >= 106 && m <= 121) {
-          constexpr int h = m - 106, f = h >> 1;
-          if constexpr (!(h & 1)) lo_x = rd_half(s_nxt, 8 + f, 0, 0);
-          else xb[f] = join(lo_x, rd_half(s_nxt, 8 + f, 0, 1));
-        }
-      }
-      if constexpr (WV == 0 && m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+      if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
       // X of tile t+1: 32 halves at MFMAs 90-121, A0 B0-B7 A1-A7 (the next iteration starts with row 0)
-      if constexpr (WV == 0 && m >= 90 && m <= 121) {
+      if constexpr (m >= 90 && m <= 121) {
         constexpr int h = m - 90;
         constexpr int ord[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};
         constexpr int f = ord[h >> 1];
@@ -364,14 +349,7 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
   ushort* c = (ushort*)C;
   float* slab = splitk > 1 ? ws : nullptr;
   const int gmr = ((flags >> 8) & 15) ? ((flags >> 8) & 15) : TH_TN_GM;  // XCD band height (tile rows)
-  const int wv = (flags >> 13) & 7;
   auto hbv = [&](bool split_, unsigned g, int sk, int t0) {
-    if (wv == 1) {
-      if (split_) gemm_tn_hb_kernel<true, false, 1><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, sk, t0, gmr);
-      else if (beta) gemm_tn_hb_kernel<false, true, 1><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
-      else gemm_tn_hb_kernel<false, false, 1><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
-      return;
-    }
     if (split_) gemm_tn_hb_kernel<true, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, sk, t0, gmr);
     else if (beta) gemm_tn_hb_kernel<false, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
     else gemm_tn_hb_kernel<false, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);

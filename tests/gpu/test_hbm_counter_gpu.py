@@ -34,6 +34,17 @@ def _tool():
     return p
 
 
+def _task_env():
+    """What th-run puts in a task's environment: the tool, and the cut-down counter definitions
+    that keep the tool's startup cost small (native/build.py::build_hbm_metrics)."""
+    from tensorhive_fixed_amd.core import hbm
+
+    _tool()
+    env = hbm.task_env()
+    assert "ROCPROFILER_METRICS_PATH" in env, "th-hbm metrics subset not generated"
+    return env
+
+
 def _sample_during(script_args, env, seconds=2.5, settle=1.2):
     from tensorhive_fixed_amd.core.telemetry import AmdSmiBackend
 
@@ -59,7 +70,7 @@ def _sample_during(script_args, env, seconds=2.5, settle=1.2):
 
 
 def test_counted_hbm_bw_tracks_a_copy_stream():
-    env = {"ROCP_TOOL_LIBRARIES": _tool(), "TH_HBM_PERIOD_MS": "500", "TENSORHIVE_TASK_ID": "1"}
+    env = {**_task_env(), "TH_HBM_PERIOD_MS": "500", "TENSORHIVE_TASK_ID": "1"}
     vals, sources, stream = _sample_during([str(ROOT / "scripts" / "hbm_stream.py"), "6", "copy"], env)
     assert vals, f"no counter-based sample (sources {sources})"
     measured = sorted(vals)[len(vals) // 2]
@@ -91,7 +102,7 @@ def _pmc_bytes_per_iter(tmp_path) -> float:
 
 def test_counted_hbm_bw_matches_dispatch_pmc_on_the_gemm_swiglu_mix(tmp_path):
     per_iter = _pmc_bytes_per_iter(tmp_path)  # bytes per iteration, rocprofv3 dispatch mode
-    env = {"ROCP_TOOL_LIBRARIES": _tool(), "TH_HBM_PERIOD_MS": "500", "TENSORHIVE_TASK_ID": "1"}
+    env = {**_task_env(), "TH_HBM_PERIOD_MS": "500", "TENSORHIVE_TASK_ID": "1"}
     vals, sources, run = _sample_during([str(ROOT / "scripts" / "hbm_mix.py"), "6"], env)
     assert vals, f"no counter-based sample (sources {sources})"
     expected = per_iter * run["iters"] / run["seconds"] / 1e9

@@ -84,7 +84,7 @@ def test_counted_task_beside_a_foreign_stream_is_partial():
     be = AmdSmiBackend(task_hbm=True)
     secs = 8
     start = {"HBM_STREAM_START_AT": f"{time.time() + 25:.3f}"}  # both streams over the same window
-    counted = _stream({"ROCP_TOOL_LIBRARIES": tool, "TH_HBM_PERIOD_MS": "500", "TENSORHIVE_TASK_ID": "77", **start},
+    counted = _stream({**hbm.task_env(), "TH_HBM_PERIOD_MS": "500", "TENSORHIVE_TASK_ID": "77", **start},
                       secs)
     foreign = _stream(start, secs)
     try:
