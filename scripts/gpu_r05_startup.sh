@@ -8,7 +8,7 @@ for i in 1 2 3; do
     unset ROCPROFILER_METRICS_PATH
     case $mode in
       plain) L="";; null) L=$R/scripts/libnulltool.so;; eager) L=$R/scripts/libthhbm_eager.so;;
-      lazy) L=$R/tensorhive_fixed_amd/native/lib/libthhbm.so;; lazym) L=$R/tensorhive_fixed_amd/native/lib/libthhbm.so; export ROCPROFILER_METRICS_PATH=$R/tensorhive_fixed_amd/native/share/th-hbm-metrics;; p1|p2|p3|p4|p5) L=$R/scripts/libprobetool${mode#p}.so;;
+      lazy) L=$R/tensorhive_fixed_amd/native/lib/libthhbm.so;;  p1|p2|p3|p4|p5) L=$R/scripts/libprobetool${mode#p}.so;;
     esac
     s=$(date +%s.%N)
     ROCP_TOOL_LIBRARIES=$L timeout -k 10 120 python -c "$J" > gpurun_out/r05/$T/$mode$i.log 2>&1 || exit 1

@@ -14,10 +14,21 @@
 #include <rocprofiler-sdk/fwd.h>
 #include <rocprofiler-sdk/registration.h>
 
+#include <stdio.h>
+#include <time.h>
+
 #include <vector>
 
 namespace {
+double now_s() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + t.tv_nsec * 1e-9;
+}
+double g_t_configure = 0;
 int init(rocprofiler_client_finalize_t, void*) {
+  const double t_init = now_s();
+  fprintf(stderr, "[probe-tool] configure -> init %.3f s\n", t_init - g_t_configure);
   if (PROBE_LEVEL < 2) return 0;
   constexpr bool kContexts = PROBE_LEVEL != 4, kBuffers = PROBE_LEVEL == 2 || PROBE_LEVEL == 3;
   std::vector<rocprofiler_agent_v0_t> agents;
@@ -31,6 +42,7 @@ int init(rocprofiler_client_finalize_t, void*) {
         return ROCPROFILER_STATUS_SUCCESS;
       },
       sizeof(rocprofiler_agent_v0_t), &agents);
+  fprintf(stderr, "[probe-tool] agent query %.3f s, %zu GPU agents\n", now_s() - t_init, agents.size());
   for (const auto& a : agents) {
     rocprofiler_context_id_t ctx{};
     rocprofiler_buffer_id_t buf{};
@@ -55,6 +67,7 @@ void fini(void*) {}
 extern "C" rocprofiler_tool_configure_result_t* rocprofiler_configure(uint32_t, const char*, uint32_t,
                                                                       rocprofiler_client_id_t* id) {
   id->name = "th-probe-tool";
+  g_t_configure = now_s();
   static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &init, &fini, nullptr};
   return &cfg;
 }

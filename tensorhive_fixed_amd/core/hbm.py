@@ -38,20 +38,9 @@ def tool_path() -> str | None:
 
 
 def task_env() -> dict[str, str]:
-    """Environment that makes a task count its own HBM traffic (empty when the tool is missing).
-
-    With the cut-down counter definitions next to the tool (``native/build.py::build_hbm_metrics``),
-    ``ROCPROFILER_METRICS_PATH`` points rocprofiler-sdk at them, so loading the tool costs the task
-    far less startup time (TH_HBM_FULL_METRICS=1 keeps the install's full set)."""
+    """Environment that makes a task count its own HBM traffic (empty when the tool is missing)."""
     p = tool_path()
-    if not p:
-        return {}
-    env = {"ROCP_TOOL_LIBRARIES": p}
-    from ..native.build import HBM_METRICS_DIR
-
-    if (HBM_METRICS_DIR / "counter_defs.yaml").exists() and os.environ.get("TH_HBM_FULL_METRICS", "0") != "1":
-        env["ROCPROFILER_METRICS_PATH"] = str(HBM_METRICS_DIR)
-    return env
+    return {"ROCP_TOOL_LIBRARIES": p} if p else {}
 
 
 def _alive(pid: int) -> bool:

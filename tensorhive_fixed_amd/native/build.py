@@ -40,7 +40,7 @@ TARGETS = {
                                           str(HERE / "th_counters.cpp"), f"-L{ROCM}/lib", "-lrocprofiler-sdk",
                                           "-lhsa-runtime64", f"-Wl,-rpath,{ROCM}/lib"]),
     "libthhbm": (LIB / "libthhbm.so", [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", f"-I{ROCM}/include",
-                                       str(HERE / "th_hbm_tool.cpp"), f"-L{ROCM}/lib", "-lrocprofiler-sdk",
+                                       str(HERE / "th_hbm_tool.cpp"), "-ldl",
                                        f"-Wl,-rpath,{ROCM}/lib"]),
     "th-probe": (BIN / "th-probe", [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", f"-I{KSRC}",
                                     str(HERE / "th_probe.hip")]),
@@ -102,41 +102,6 @@ def path_of(name: str) -> Path:
     return TARGETS[name][0]
 
 
-# Counters the in-task HBM tool reads (th_hbm_tool.cpp kCounters) and the base counters they reduce.
-HBM_TOOL_COUNTERS = ("TCC_EA0_RDREQ", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_128B", "TCC_EA0_RDREQ_128B_sum",
-                     "TCC_EA0_WRREQ", "TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B", "TCC_EA0_WRREQ_64B_sum",
-                     "GRBM_GUI_ACTIVE", "GRBM_COUNT")
-HBM_METRICS_DIR = HERE / "share" / "th-hbm-metrics"
-ROCPROF_COUNTER_DEFS = Path(ROCM) / "share" / "rocprofiler-sdk" / "counter_defs.yaml"
-
-
-def build_hbm_metrics(force: bool = False) -> Path | None:
-    """``share/th-hbm-metrics/counter_defs.yaml``: ROCm's rocprofiler-sdk counter definitions cut down to
-    the counters libthhbm reads.  A task started with the tool loads rocprofiler-sdk, whose agent
-    discovery parses every counter definition of the install for every GPU of the node; that costs
-    the task ~3.3 s of its startup (`import torch` 1.5 -> 4.8 s, profiles/r05_daemon/startup.txt).
-    ``ROCPROFILER_METRICS_PATH`` pointing here (``core/hbm.py::task_env``) makes it parse these 10
-    instead of 803.  Generated from the installed file, so event numbers always match the install."""
-    out = HBM_METRICS_DIR / "counter_defs.yaml"
-    if not ROCPROF_COUNTER_DEFS.exists():
-        return None
-    if not force and out.exists() and out.stat().st_mtime >= ROCPROF_COUNTER_DEFS.stat().st_mtime:
-        return out
-    import yaml
-
-    doc = yaml.safe_load(ROCPROF_COUNTER_DEFS.read_text())
-    root = doc["rocprofiler-sdk"]
-    keep = [c for c in root["counters"] if c.get("name") in HBM_TOOL_COUNTERS]
-    if not any(c["name"] == "TCC_EA0_RDREQ_sum" for c in keep):
-        return None
-    out.parent.mkdir(parents=True, exist_ok=True)
-    tmp = out.with_name(out.name + ".tmp")
-    tmp.write_text(yaml.safe_dump({"rocprofiler-sdk": {"counters-schema-version": root.get("counters-schema-version", 1),
-                                                       "counters": keep}}, sort_keys=False))
-    os.replace(tmp, out)
-    return out
-
-
 def _build_one(name: str, force: bool) -> tuple[str, str | None]:
     out, cmd = TARGETS[name]
     srcs = [Path(c) for c in cmd if c.endswith((".cpp", ".hip"))] + \
@@ -157,10 +122,6 @@ def _build_one(name: str, force: bool) -> tuple[str, str | None]:
 def build_all(force: bool = False, strict: bool = True) -> dict[str, str | None]:
     with cf.ThreadPoolExecutor(max_workers=4) as ex:
         results = dict(ex.map(lambda n: _build_one(n, force), [n for n in TARGETS if n not in SANITIZED]))
-    try:
-        build_hbm_metrics(force)
-    except Exception as e:  # noqa: BLE001 -- the tool then runs on the full definitions
-        print(f"[native] th-hbm metrics subset not generated: {e}", file=sys.stderr)
     errs = {k: v for k, v in results.items() if v}
     for k, v in errs.items():
         print(f"[native] {k}: FAILED\n{v}", file=sys.stderr)

@@ -26,6 +26,15 @@
 // (the LOCAL_RANK-th visible one, as the payload binds cuda:LOCAL_RANK); TH_HBM_ALL_AGENTS=1
 // samples every visible GPU (th_hbm_select.h).
 //
+// Startup cost: the library has NO DT_NEEDED entry on librocprofiler-sdk.  Every rocprofiler_* call goes
+// through a table resolved with dlsym(RTLD_DEFAULT) from the SDK copy that is already loaded when
+// rocprofiler_configure runs.  A tool that links the SDK makes rocprofiler-sdk ELF-parse EVERY library
+// loaded in the process for a rocprofiler_configure symbol, during the task's HIP initialisation.  Under
+// torch that is 66 libraries and 3.1-3.3 s added to `import torch` (1.5 -> 4.8 s; libmagma alone 1.2 s),
+// i.e. to every task's startup.  Without the link only the listed library is searched
+// (profiles/r05_daemon/startup.txt).  The counter configs (enumerating the agent's counters) are built on
+// the sampler thread, not inside tool_init.
+//
 // Validated on MI355X (profiles/r03_counters/): copy stream 4.79 TB/s counted vs 4.785 moved;
 // add stream 5.87 vs 5.76; the GEMM + SwiGLU mix 4.27 GB per iteration vs 4.04 from rocprofv3
 // dispatch-mode PMC of the same counters.
@@ -37,6 +46,7 @@
 #include <rocprofiler-sdk/device_counting_service.h>
 #include <rocprofiler-sdk/fwd.h>
 #include <rocprofiler-sdk/registration.h>
+#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -57,6 +67,39 @@ namespace {
 
 const char* const kCounters[] = {"TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_WRREQ_sum",
                                  "TCC_EA0_WRREQ_64B_sum"};
+
+// rocprofiler-sdk entry points, resolved at configure time (see the startup-cost note above)
+struct Api {
+  decltype(&rocprofiler_iterate_agent_supported_counters) iterate_counters = nullptr;
+  decltype(&rocprofiler_query_counter_info) counter_info = nullptr;
+  decltype(&rocprofiler_create_counter_config) create_counter_config = nullptr;
+  decltype(&rocprofiler_query_available_agents) query_agents = nullptr;
+  decltype(&rocprofiler_create_context) create_context = nullptr;
+  decltype(&rocprofiler_create_buffer) create_buffer = nullptr;
+  decltype(&rocprofiler_configure_device_counting_service) configure_device_counting = nullptr;
+  decltype(&rocprofiler_start_context) start_context = nullptr;
+  decltype(&rocprofiler_stop_context) stop_context = nullptr;
+  decltype(&rocprofiler_sample_device_counting_service) sample = nullptr;
+  decltype(&rocprofiler_query_record_counter_id) record_counter_id = nullptr;
+
+  template <typename F>
+  static bool get(F& f, const char* name) {
+    f = reinterpret_cast<F>(dlsym(RTLD_DEFAULT, name));
+    return f != nullptr;
+  }
+  bool resolve() {
+    return get(iterate_counters, "rocprofiler_iterate_agent_supported_counters") &&
+           get(counter_info, "rocprofiler_query_counter_info") &&
+           get(create_counter_config, "rocprofiler_create_counter_config") &&
+           get(query_agents, "rocprofiler_query_available_agents") &&
+           get(create_context, "rocprofiler_create_context") && get(create_buffer, "rocprofiler_create_buffer") &&
+           get(configure_device_counting, "rocprofiler_configure_device_counting_service") &&
+           get(start_context, "rocprofiler_start_context") && get(stop_context, "rocprofiler_stop_context") &&
+           get(sample, "rocprofiler_sample_device_counting_service") &&
+           get(record_counter_id, "rocprofiler_query_record_counter_id");
+  }
+};
+Api g_api;
 
 struct Agent {
   rocprofiler_agent_v0_t info{};
@@ -86,7 +129,7 @@ std::string bdf_of(const rocprofiler_agent_v0_t& a) {
 
 void configure(Agent* a) {
   std::vector<rocprofiler_counter_id_t> ids;
-  rocprofiler_iterate_agent_supported_counters(
+  g_api.iterate_counters(
       a->info.id,
       [](rocprofiler_agent_id_t, rocprofiler_counter_id_t* c, size_t n, void* ud) {
         static_cast<std::vector<rocprofiler_counter_id_t>*>(ud)->insert(
@@ -97,7 +140,7 @@ void configure(Agent* a) {
   std::unordered_map<std::string, rocprofiler_counter_id_t> by_name;
   for (auto id : ids) {
     rocprofiler_counter_info_v0_t info;
-    if (rocprofiler_query_counter_info(id, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) == ROCPROFILER_STATUS_SUCCESS)
+    if (g_api.counter_info(id, ROCPROFILER_COUNTER_INFO_VERSION_0, &info) == ROCPROFILER_STATUS_SUCCESS)
       by_name.emplace(info.name, id);
   }
   std::vector<rocprofiler_counter_id_t> want;
@@ -107,16 +150,16 @@ void configure(Agent* a) {
     want.push_back(it->second);
     a->names.emplace(it->second.handle, n);
     rocprofiler_counter_info_v1_t info1;
-    if (rocprofiler_query_counter_info(it->second, ROCPROFILER_COUNTER_INFO_VERSION_1, &info1) ==
+    if (g_api.counter_info(it->second, ROCPROFILER_COUNTER_INFO_VERSION_1, &info1) ==
         ROCPROFILER_STATUS_SUCCESS)
       a->n_records += info1.dimensions_instances_count;
   }
-  if (!want.empty()) rocprofiler_create_counter_config(a->info.id, want.data(), want.size(), &a->config);
+  if (!want.empty()) g_api.create_counter_config(a->info.id, want.data(), want.size(), &a->config);
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
   std::vector<rocprofiler_agent_v0_t> agents;
-  rocprofiler_query_available_agents(
+  g_api.query_agents(
       ROCPROFILER_AGENT_INFO_VERSION_0,
       [](rocprofiler_agent_version_t, const void** arr, size_t n, void* ud) {
         for (size_t i = 0; i < n; ++i) {
@@ -138,8 +181,8 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
   for (const auto& info : chosen) {
     auto* a = new Agent();
     a->info = info;
-    if (rocprofiler_create_context(&a->ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
-    if (rocprofiler_create_buffer(
+    if (g_api.create_context(&a->ctx) != ROCPROFILER_STATUS_SUCCESS) continue;
+    if (g_api.create_buffer(
             a->ctx, 4096, 2048, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
             [](rocprofiler_context_id_t, rocprofiler_buffer_id_t, rocprofiler_record_header_t**, size_t, void*,
                uint64_t) {},
@@ -149,7 +192,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     // seconds, and tool_init runs inside the task's HSA initialisation (its `import torch`), so every
     // task would start that much later (profiles/r05_daemon/startup.txt).  The service only needs the
     // config when a context starts; the sampler thread builds it first.
-    if (rocprofiler_configure_device_counting_service(
+    if (g_api.configure_device_counting(
             a->ctx, a->buf, info.id,
             [](rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_device_counting_agent_cb_t set,
                void* ud) {
@@ -196,7 +239,7 @@ void sampler() {
   }
   g_agents.swap(live);
   while (!g_stop && !g_agents.empty()) {
-    for (auto* a : g_agents) rocprofiler_start_context(a->ctx);
+    for (auto* a : g_agents) g_api.start_context(a->ctx);
     const uint64_t t0 = now_ns();
     for (int slept = 0; slept < period_ms && !g_stop; slept += 10) usleep(10000);
     const double window_ms = (now_ns() - t0) / 1e6;
@@ -207,16 +250,16 @@ void sampler() {
       std::vector<rocprofiler_counter_record_t> rec(a->n_records + 64);
       size_t n = rec.size();
       std::map<std::string, double> sums;
-      if (rocprofiler_sample_device_counting_service(a->ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, rec.data(), &n) ==
+      if (g_api.sample(a->ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, rec.data(), &n) ==
           ROCPROFILER_STATUS_SUCCESS) {
         for (size_t r = 0; r < n; ++r) {
           rocprofiler_counter_id_t cid{};
-          rocprofiler_query_record_counter_id(rec[r].id, &cid);
+          g_api.record_counter_id(rec[r].id, &cid);
           auto it = a->names.find(cid.handle);
           if (it != a->names.end()) sums[it->second] += rec[r].counter_value;
         }
       }
-      rocprofiler_stop_context(a->ctx);
+      g_api.stop_context(a->ctx);
       const double rd = sums["TCC_EA0_RDREQ_sum"], rd128 = sums["TCC_EA0_RDREQ_128B_sum"];
       const double wr = sums["TCC_EA0_WRREQ_sum"], wr64 = sums["TCC_EA0_WRREQ_64B_sum"];
       const double rd_bytes = 128.0 * rd128 + 64.0 * (rd - rd128 > 0 ? rd - rd128 : 0);
@@ -259,6 +302,7 @@ int tool_init_and_start(rocprofiler_client_finalize_t fini, void* data) {
 extern "C" rocprofiler_tool_configure_result_t* rocprofiler_configure(uint32_t, const char*, uint32_t,
                                                                       rocprofiler_client_id_t* id) {
   id->name = "th-hbm";
+  if (!g_api.resolve()) return nullptr;  // no SDK loaded in this process: nothing to count with
   static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &tool_init_and_start,
                                                  &tool_fini, nullptr};
   return &cfg;
