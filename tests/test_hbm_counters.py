@@ -1,4 +1,5 @@
 """In-task HBM counters (core/hbm.py): per-GPU rates from the tool's per-process files, stale and
+import pytest
 dead-process files ignored (dead ones removed), and th-run tasks on the local node carry the tool."""
 import json
 import os
@@ -39,3 +40,23 @@ def test_local_tasks_get_the_counter_tool(cfg, monkeypatch):
     assert task_nursery.spawn_env("localnode") == {}
     cmd = task_nursery.build_spawn_command("python t.py", 7, "th-run", {"ROCP_TOOL_LIBRARIES": "/x.so"})
     assert "--env ROCP_TOOL_LIBRARIES=/x.so" in cmd and "--env TENSORHIVE_TASK_ID=7" in cmd
+
+
+def test_task_tool_does_not_link_the_profiler_sdk():
+    """libthhbm must not carry a DT_NEEDED entry on librocprofiler-sdk: a tool that links it makes
+    rocprofiler-sdk ELF-parse every library loaded in the task at HIP initialisation (+3.3 s per task
+    under torch, profiles/r05_daemon/README.md); the tool resolves the SDK's entry points with dlsym."""
+    import shutil
+    import subprocess
+
+    from tensorhive_fixed_amd.native.build import _build_one, path_of
+
+    if shutil.which("readelf") is None:
+        pytest.skip("readelf not available")
+    name, err = _build_one("libthhbm", False)
+    if err:
+        pytest.skip(f"libthhbm not buildable here: {err[:200]}")
+    out = subprocess.run(["readelf", "-d", str(path_of("libthhbm"))], capture_output=True, text=True, check=True).stdout
+    needed = [ln for ln in out.splitlines() if "(NEEDED)" in ln]
+    assert needed, out
+    assert not any("rocprofiler" in ln for ln in needed), needed
