@@ -1,9 +1,10 @@
 """In-task HBM counters (core/hbm.py): per-GPU rates from the tool's per-process files, stale and
-import pytest
 dead-process files ignored (dead ones removed), and th-run tasks on the local node carry the tool."""
 import json
 import os
 import time
+
+import pytest
 
 from tensorhive_fixed_amd.core import hbm
 
