@@ -5,22 +5,29 @@ kernel's output straight to BOTH consumers in the layout each GEMM wants (``ops/
 ``profiles/r01_gemm/``):
 
 * ``dH = dGU @ W13`` -- ``dGU`` row-major, W13 transposed once (K-contiguous "NT" form);
-* ``dW13 = dGUᵀ @ H`` -- run as ``(dGUᵀ) @ (Hᵀ)ᵀ`` on ``dGUᵀ`` written directly by the
-  ``th_swiglu_bwd_t`` kernel (one extra write of 2F x T bf16 instead of a separate transpose pass
-  of 1.1 ms per layer at 32k tokens) and ``Hᵀ`` from the transpose kernel.
+* ``dW13 = dGUᵀ @ H`` -- by default on the gfx950 TN kernel (``ops/gemm_tn.py``) straight from ``dGU`` and
+  ``H`` as they are: 6.38 ms per layer with the plain SwiGLU backward against 6.60 for the previous path
+  (``TH_W13_WGRAD_TN=0``: ``(dGUᵀ) @ (Hᵀ)ᵀ`` on hipBLASLt, with ``dGUᵀ`` written by the ``th_swiglu_bwd_t``
+  kernel and ``Hᵀ`` from the transpose kernel; ``profiles/r05_gemm/w13_wgrad_paths.jsonl``).
 
 On the CPU (unit tests) the same math runs in PyTorch.  ``F % 64 != 0`` falls back to the
 unfused pair on the GPU.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
 from ._grad import deliver, mm_into, nt_into, nt_mm
-from .linear import _DGRAD_NT, linear
+from .gemm_tn import gemm_tn_, supported as _tn_supported
+from .linear import _DGRAD_NT, linear, tn_into
 from .swiglu import swiglu, swiglu_reference
 from .transpose import transpose
+
+
+_W13_TN = os.environ.get("TH_W13_WGRAD_TN", "1") == "1"
 
 
 class _GateUpSwiGLU(torch.autograd.Function):
@@ -49,7 +56,14 @@ class _GateUpSwiGLU(torch.autograd.Function):
         d2 = da.reshape(T, F)
         if not d2.is_contiguous():
             d2 = d2.contiguous()
-        if gu.is_cuda:
+        if gu.is_cuda and _W13_TN and _tn_supported(F2, h2.shape[1], T):
+            dgu = torch.empty_like(gu)
+            _lib.call("th_swiglu_bwd", d2.data_ptr(), gu.data_ptr(), dgu.data_ptr(), T, F, _lib.stream_ptr(gu.device))
+            dh = nt_mm(dgu, transpose(w13)) if _DGRAD_NT else torch.mm(dgu, w13)
+            gw = deliver(w13, tn_into(dgu, h2),
+                         lambda: gemm_tn_(dgu, h2, torch.empty(w13.shape, device=gu.device, dtype=gu.dtype)))
+            del dgu
+        elif gu.is_cuda:
             dgu = torch.empty_like(gu)
             dguT = torch.empty((F2, T), device=gu.device, dtype=gu.dtype)
             _lib.call("th_swiglu_bwd_t", d2.data_ptr(), gu.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), T, F,

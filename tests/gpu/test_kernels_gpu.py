@@ -204,10 +204,15 @@ def test_swiglu_bwd_transposed_output(T, F):
     assert torch.equal(dguT, dgu.t())
 
 
-def test_gate_up_swiglu_matches_unfused():
+@pytest.mark.parametrize("w13_tn", [True, False])
+def test_gate_up_swiglu_matches_unfused(w13_tn, monkeypatch):
+    """Both weight-gradient paths of the fused gate|up + SwiGLU node: the TN kernel on dGU and H (default),
+    and hipBLASLt on dGU^T (written by the transposing SwiGLU backward) and H^T."""
+    from tensorhive_fixed_amd.ops import mlp
     from tensorhive_fixed_amd.ops.linear import linear
     from tensorhive_fixed_amd.ops.mlp import gate_up_swiglu
     from tensorhive_fixed_amd.ops.swiglu import swiglu
+    monkeypatch.setattr(mlp, "_W13_TN", w13_tn)
     torch.manual_seed(10)
     T, D, F = 512, 256, 512
     h = torch.randn(T, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
