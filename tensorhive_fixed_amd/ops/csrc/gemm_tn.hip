@@ -51,6 +51,25 @@ __device__ __forceinline__ void static_for_tn(F&& f) {
     static_for_tn<I + 1, N>(f);
   }
 }
+// Diagnostic build only (-DTH_TN_DIAG=1: scripts/build_variant_lib.sh tn_diag -DTH_TN_DIAG=1 gemm_tn,
+// scripts/tn_stamps.py): s_memtime stamps around the three waits of each k-tile, summed per wave and added
+// into g_tn_stamp = {k-tiles, whole loop, barrier 20, barrier 44, vmcnt + barrier 88} (shader cycles).
+// The production libthk.so has none of it.
+#ifdef TH_TN_DIAG
+__device__ unsigned long long g_tn_stamp[8];
+__device__ __forceinline__ unsigned long long tn_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+constexpr bool kTnDiag = true;
+#else
+__device__ __forceinline__ unsigned long long tn_stamp() { return 0; }
+constexpr bool kTnDiag = false;
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // Schedule "hb": one wave per SIMD, the machine of hipBLASLt's NT kernels (and of the NT kernel's hb
 // schedule, removed in round 5: profiles/r05_gemm/gemm_nt_removed.patch), on the TN operands:
@@ -174,6 +193,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     return __builtin_bit_cast(bf16x8, v);
   };
   i16x4 lo_y = {0, 0, 0, 0}, lo_x = {0, 0, 0, 0};
+  unsigned long long d_loop = 0, d_w[3] = {0, 0, 0}, d_t = 0;
+  if constexpr (kTnDiag) d_loop = tn_stamp();
   for (int t = 0; t < nt; ++t) {
     const int st = t & 1;
     const int kt2 = min(t + 2, nt - 1);  // past the end: re-stage the last tile (nobody reads it)
@@ -191,6 +212,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
         if constexpr (!(m & 1)) lo_y = rd_half(s_cur, m >> 1, 1, 0);
         else ya[m >> 1] = join(lo_y, rd_half(s_cur, m >> 1, 1, 1));
       }
+      if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_t = tn_stamp();
       if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       // DMA pieces spread over the whole k-tile: A's 8 every 4th MFMA from 22 (after the barrier that
       // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
@@ -206,6 +228,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece(1, (m - b0) / bs, kt2, st);
       if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+      if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_w[m == 20 ? 0 : m == 44 ? 1 : 2] += tn_stamp() - d_t;
       // X of tile t+1: 32 halves at MFMAs 90-121, A0 B0-B7 A1-A7 (the next iteration starts with row 0)
       if constexpr (m >= 90 && m <= 121) {
         constexpr int h = m - 90;
@@ -222,6 +245,14 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       __builtin_amdgcn_sched_barrier(0);
     });
   }
+#ifdef TH_TN_DIAG
+  if (lane == 0) {
+    const unsigned long long loop = tn_stamp() - d_loop;
+    atomicAdd(&g_tn_stamp[0], (unsigned long long)nt);
+    atomicAdd(&g_tn_stamp[1], loop);
+    for (int i = 0; i < 3; ++i) atomicAdd(&g_tn_stamp[2 + i], d_w[i]);
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier\n\ts_nop 15\n\ts_nop 15" ::: "memory");
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -375,3 +406,14 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
   }
   TH_CHECK_LAUNCH();
 }
+
+#ifdef TH_TN_DIAG
+// g_tn_stamp -> buf[8]; reset != 0 zeroes it instead
+extern "C" int th_tn_stamps(unsigned long long* buf, int reset) {
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tn_stamp), z, sizeof z) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_tn_stamp), 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
