@@ -140,9 +140,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem_raw;
   const ushort* ga = A + kbeg * lda + m0;
   const ushort* gb = B + kbeg * ldb + n0;
-  auto piece = [&](int op, int i, int kt, int st) {
+  // piece i of operand op of the k-tile whose first k-row is at `base`, into stage st
+  auto piece_at = [&](int op, int i, const ushort* base, int st) {
     const long ld = op == 0 ? lda : ldb;
-    const ushort* base = (op == 0 ? ga : gb) + (long)kt * 64 * ld;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
     const int u = 4 * i + w;
     const unsigned soff = (unsigned)(2L * 2 * u * ld);
@@ -150,6 +150,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const unsigned lb = __builtin_amdgcn_readfirstlane(lds0 + st * HSTAGE + op * HIMG + u * 1024);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :: "s"(lb), "v"(voff), "s"(r), "s"(soff) : "memory", "m0");
+  };
+  auto piece = [&](int op, int i, int kt, int st) {
+    piece_at(op, i, (op == 0 ? ga : gb) + (long)kt * 64 * (op == 0 ? lda : ldb), st);
   };
 
   f32x4 acc[8][8];
@@ -195,9 +198,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   i16x4 lo_y = {0, 0, 0, 0}, lo_x = {0, 0, 0, 0};
   unsigned long long d_loop = 0, d_w[3] = {0, 0, 0}, d_t = 0;
   if constexpr (kTnDiag) d_loop = tn_stamp();
+  // k-tile t+2's first rows, advanced incrementally (no 64-bit multiply per k-tile); past the end the last
+  // tile is re-staged (nobody reads it)
+  const ushort* pa2 = ga + (long)min(2, nt - 1) * 64 * lda;
+  const ushort* pb2 = gb + (long)min(2, nt - 1) * 64 * ldb;
   for (int t = 0; t < nt; ++t) {
     const int st = t & 1;
-    const int kt2 = min(t + 2, nt - 1);  // past the end: re-stage the last tile (nobody reads it)
     const char LDS_AS* s_cur = smem + st * HSTAGE;
     const char LDS_AS* s_nxt = smem + (st ^ 1) * HSTAGE;
     static_for_tn<0, 128>([&](auto mc) {
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
       // (2 % faster than A every 2nd from 22 and B every 4th from 46: profiles/r05_gemm/tn_pv_sweep*.jsonl)
       constexpr int a0 = 22, as = 4, b0 = 52, bs = 5;
-      if constexpr (m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0) piece(0, (m - a0) / as, kt2, st);
+      if constexpr (m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0) piece_at(0, (m - a0) / as, pa2, st);
       // Y.b: 16 halves at MFMAs 23-38
       if constexpr (m >= 23 && m <= 38) {
         constexpr int h = m - 23;
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
         else yb[h >> 1] = join(lo_y, rd_half(s_cur, 8 + (h >> 1), 1, 1));
       }
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece(1, (m - b0) / bs, kt2, st);
+      if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece_at(1, (m - b0) / bs, pb2, st);
       if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_w[m == 20 ? 0 : m == 44 ? 1 : 2] += tn_stamp() - d_t;
       // X of tile t+1: 32 halves at MFMAs 90-121, A0 B0-B7 A1-A7 (the next iteration starts with row 0)
@@ -244,6 +250,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
     });
+    if (t + 3 < nt) {
+      pa2 += 64 * lda;
+      pb2 += 64 * ldb;
+    }
   }
 #ifdef TH_TN_DIAG
   if (lane == 0) {
