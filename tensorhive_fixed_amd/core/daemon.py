@@ -79,6 +79,8 @@ class Daemon:
         self._topology_cache: dict = {}
         self._lock = threading.Lock()
         self.task_events: list[tuple[float, str, dict]] = []  # (unix time, host, event), newest last
+        self._event_sampled: dict[str, float] = {}  # host -> time of its last event-triggered sample
+        self._event_deferred: dict[str, threading.Timer] = {}  # host -> its pending trailing sample
         self.events = None
         self._start_task_events()
 
@@ -121,13 +123,40 @@ class Daemon:
             return self.cfg.launcher.node_events_socket or None
         return None
 
+    # a host is re-sampled for task events at most this often: the node socket takes datagrams from any
+    # local user, so a flood must not turn into a flood of telemetry samples (the wake is coalesced anyway)
+    EVENT_SAMPLE_MIN_S = 0.02
+
     def on_task_event(self, host: str, ev: dict) -> None:
         """A task on ``host`` ended: refresh that host's telemetry now (its devices no longer show
         the task's processes) and run the job scheduler, which releases the devices and starts the
         next queued job in the same tick."""
+        now = time.time()
         with self._lock:
-            self.task_events.append((time.time(), host, dict(ev)))
+            self.task_events.append((now, host, dict(ev)))
             del self.task_events[:-256]
+            wait = self._event_sampled.get(host, 0.0) + self.EVENT_SAMPLE_MIN_S - now
+            if wait <= 0:
+                self._event_sampled[host] = now
+            elif host in self._event_deferred:
+                return  # a trailing sample + wake for this host is already scheduled
+            else:
+                # inside the window: one trailing sample + wake at its end, so a real exit that follows
+                # another event closely is still seen at once
+                t = threading.Timer(wait, self._deferred_task_event, args=(host,))
+                t.daemon = True
+                self._event_deferred[host] = t
+                t.start()
+                return
+        self._sample_and_wake(host)
+
+    def _deferred_task_event(self, host: str) -> None:
+        with self._lock:
+            self._event_deferred.pop(host, None)
+            self._event_sampled[host] = time.time()
+        self._sample_and_wake(host)
+
+    def _sample_and_wake(self, host: str) -> None:
         from .services import MonitoringService
 
         mon = self.service(MonitoringService)
@@ -188,6 +217,10 @@ class Daemon:
         if self.events is not None:
             self.events.close()
             self.events = None
+        with self._lock:
+            pending, self._event_deferred = list(self._event_deferred.values()), {}
+        for t in pending:
+            t.cancel()
         for s in self.services:
             s.stop()
         for s in self.services:

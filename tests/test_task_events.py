@@ -150,3 +150,26 @@ def test_agent_forwards_exit_events(tmp_path):
         p.terminate()
         p.wait(10)
     assert not os.path.exists(sock)
+
+
+def test_an_event_flood_is_not_a_sampling_flood(world, monkeypatch):
+    """The node socket takes datagrams from any local user: 200 events in a burst re-sample the host
+    (and wake the scheduler) a bounded number of times -- at most once per Daemon.EVENT_SAMPLE_MIN_S,
+    plus one trailing sample at the end of the burst, so the last event is never left unseen."""
+    from tensorhive_fixed_amd.core.services import MonitoringService
+
+    d, _, _ = world
+    mon = MonitoringService(3600.0, d.backends)
+    d.add_service(mon)
+    samples, wakes = [], []
+    monkeypatch.setattr(mon, "sample_host", lambda host: samples.append(host))
+    monkeypatch.setattr(d, "wake", lambda reason="": wakes.append(reason))
+    t0 = time.time()
+    for i in range(200):
+        d.on_task_event("node-a", {"event": "task_exit", "name": f"x{i}"})
+    elapsed = time.time() - t0
+    time.sleep(3 * d.EVENT_SAMPLE_MIN_S)  # the trailing sample of the burst
+    assert len(d.task_events) == 200
+    assert 2 <= len(samples) <= 3 + int(elapsed / d.EVENT_SAMPLE_MIN_S)
+    assert len(samples) == len(wakes) and len(samples) < 50
+    assert time.time() - t0 < 2.0
