@@ -36,6 +36,9 @@ import socket
 import sys
 import time
 
+EVENT_MIN_GAP_S = 0.02  # minimum time between an event-triggered sample and the previous sample
+MAX_EVENTS_PER_SAMPLE = 64  # task-exit events forwarded with one sample (a flood's excess is dropped)
+
 
 def _stub_backend(args):
     from .core.telemetry import StubBackend
@@ -135,12 +138,17 @@ def main(argv: list[str] | None = None) -> int:
 
                     from .core.events import parse_event
 
-                    r, _, _ = select.select([ev_sock], [], [], min(left, 0.05))
+                    # an event samples the node at once, but not sooner than EVENT_MIN_GAP_S after the last
+                    # sample: any local user can send to the socket, so a flood coalesces into one sample
+                    since = time.monotonic() - t0
+                    wait = min(left, 0.05) if not events else max(0.0, EVENT_MIN_GAP_S - since)
+                    if events and wait == 0.0:
+                        break  # sample now
+                    r, _, _ = select.select([ev_sock], [], [], wait)
                     if r:
                         ev = parse_event(ev_sock.recv(65536))
-                        if ev is not None:
+                        if ev is not None and len(events) < MAX_EVENTS_PER_SAMPLE:
                             events.append(ev)
-                            break  # sample now
                 else:
                     time.sleep(min(left, 0.05))
                 left = period - (time.monotonic() - t0)

@@ -173,3 +173,39 @@ def test_an_event_flood_is_not_a_sampling_flood(world, monkeypatch):
     assert 2 <= len(samples) <= 3 + int(elapsed / d.EVENT_SAMPLE_MIN_S)
     assert len(samples) == len(wakes) and len(samples) < 50
     assert time.time() - t0 < 2.0
+
+
+def test_agent_coalesces_an_event_flood(tmp_path):
+    """A burst of 300 datagrams at the node agent turns into a bounded number of samples (one per
+    agent.EVENT_MIN_GAP_S at most) and at most agent.MAX_EVENTS_PER_SAMPLE events per sample."""
+    import threading
+
+    from tensorhive_fixed_amd import agent
+
+    sock = str(tmp_path / "ev.sock")
+    p = subprocess.Popen([sys.executable, "-m", "tensorhive_fixed_amd.agent", "--stream", "5000", "--backend", "stub",
+                          "--stub-gpus", "1", "--host", "n9", "--events", sock], stdout=subprocess.PIPE, text=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        assert "entry" in json.loads(p.stdout.readline())
+        t0 = time.time()
+        while not os.path.exists(sock) and time.time() - t0 < 10:
+            time.sleep(0.02)
+        c = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
+        t_send = time.time()
+        for i in range(300):
+            c.sendto(json.dumps({"event": "task_exit", "name": f"t{i}"}).encode(), sock)
+        burst = time.time() - t_send
+        lines: list[dict] = []
+        reader = threading.Thread(target=lambda: [lines.append(json.loads(ln)) for ln in p.stdout], daemon=True)
+        reader.start()
+        time.sleep(1.0)
+        docs = list(lines)
+        entries = sum("entry" in d for d in docs)
+        events = sum("event" in d for d in docs)
+        assert events >= 1
+        assert entries <= 3 + int((burst + 1.0) / agent.EVENT_MIN_GAP_S)
+        assert events <= entries * agent.MAX_EVENTS_PER_SAMPLE
+    finally:
+        p.terminate()
+        p.wait(10)
