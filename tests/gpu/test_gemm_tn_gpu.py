@@ -59,3 +59,29 @@ def test_gemm_tn_data_parallel_plus_remainder_split(accumulate, band):
     torch.cuda.synchronize()
     err = (out.float() - ref).abs().max().item()
     assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("name,M,N,K,accumulate", [
+    ("wqkv", 6144, 4096, 32768, False),
+    ("wo", 4096, 4096, 32768, False),
+    ("w13", 28672, 4096, 32768, False),
+    ("w2", 4096, 14336, 32768, False),
+    ("lm_head_chunk", 128256 // 256 * 256, 4096, 4096, True),
+])
+def test_gemm_tn_llama_wgrad_shapes_match_fp32(name, M, N, K, accumulate):
+    """Every weight-gradient shape of the Llama-3-8B step (32768 tokens; the LM head per 4096-token chunk,
+    accumulating) with the default launch (mode 10, default split-K) against an fp32 reference."""
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16, generator=g)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    out = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g) if accumulate else \
+        torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ref = a.float().t() @ b.float()
+    if accumulate:
+        ref += out.float()
+    gemm_tn_(a, b, out, accumulate=accumulate)
+    torch.cuda.synchronize()
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    assert rel < 5e-3, (name, rel)
+    del a, b, out, ref
+    torch.cuda.empty_cache()
