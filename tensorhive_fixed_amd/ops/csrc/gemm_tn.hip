@@ -86,7 +86,7 @@ constexpr bool kTnDiag = false;
 //              | 44 barrier;  52- 87 DMA B of tile t+2 (8 pieces, every 5th MFMA)
 //       MFMA  64-127  k-step 1 (Y); 88: vmcnt(16) + barrier (tile t+1 landed); 90-121 read X of tile t+1
 //   * epilogue: bf16 through LDS with 16-B row stores (beta: C added), or f32x4 stores into the split-K slab.
-template <bool SPLIT, bool BETA, bool STAG = false>
+template <bool SPLIT, bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
     ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int tile0,
@@ -223,14 +223,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       // DMA pieces spread over the whole k-tile: A's 8 every 4th MFMA from 22 (after the barrier that
       // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
       // (2 % faster than A every 2nd from 22 and B every 4th from 46: profiles/r05_gemm/tn_pv_sweep*.jsonl)
-      constexpr int a0 = 22, as = 4, b0 = STAG ? 48 : 52, bs = 5;
-      if constexpr (!STAG) {
-        if constexpr (m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0) piece_at(0, (m - a0) / as, pa2, st);
-      } else if constexpr (m >= a0 && m < a0 + 8 * as) {
-        // staggered: wave w issues its piece k (0-7) at a0 + as k + w, one wave per slot (TA queue)
-        static_assert((m - a0) / as < 8, "A piece index out of range");
-        if (w == (m - a0) % as) piece_at(0, (m - a0) / as, pa2, st);
-      }
+      constexpr int a0 = 22, as = 4, b0 = 52, bs = 5;
+      if constexpr (m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0) piece_at(0, (m - a0) / as, pa2, st);
       // Y.b: 16 halves at MFMAs 23-38
       if constexpr (m >= 23 && m <= 38) {
         constexpr int h = m - 23;
@@ -238,12 +232,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
         else yb[h >> 1] = join(lo_y, rd_half(s_cur, 8 + (h >> 1), 1, 1));
       }
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if constexpr (!STAG) {
-        if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece_at(1, (m - b0) / bs, pb2, st);
-      } else if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs < 4) {
-        static_assert((m - b0) / bs < 8 && m < 88, "B piece index or slot out of range");
-        if (w == (m - b0) % bs) piece_at(1, (m - b0) / bs, pb2, st);
-      }
+      if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece_at(1, (m - b0) / bs, pb2, st);
       if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_w[m == 20 ? 0 : m == 44 ? 1 : 2] += tn_stamp() - d_t;
       // X of tile t+1: 32 halves at MFMAs 90-121, A0 B0-B7 A1-A7 (the next iteration starts with row 0)
@@ -401,14 +390,7 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
   ushort* c = (ushort*)C;
   float* slab = splitk > 1 ? ws : nullptr;
   const int gmr = ((flags >> 8) & 15) ? ((flags >> 8) & 15) : TH_TN_GM;  // XCD band height (tile rows)
-  const bool stag = flags & 8192;
   auto hbv = [&](bool split_, unsigned g, int sk, int t0) {
-    if (stag) {
-      if (split_) gemm_tn_hb_kernel<true, false, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, sk, t0, gmr);
-      else if (beta) gemm_tn_hb_kernel<false, true, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
-      else gemm_tn_hb_kernel<false, false, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
-      return;
-    }
     if (split_) gemm_tn_hb_kernel<true, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, sk, t0, gmr);
     else if (beta) gemm_tn_hb_kernel<false, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
     else gemm_tn_hb_kernel<false, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);

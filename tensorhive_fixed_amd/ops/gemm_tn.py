@@ -42,13 +42,11 @@ def default_splitk(m: int, n: int, k: int, cus: int = 256) -> int:
 # were retired, profiles/r05_gemm/): 9 = whole-K tiles, or split-K for every tile when splitk > 1;
 # 10 = whole tiles data-parallel on every CU, split-K only for the remainder tiles
 _MODES = {9: 64, 10: 192}
-_STAG = os.environ.get("TH_GEMM_TN_STAGGER", "0") == "1"  # per-wave staggered DMA pieces (launch flags bit 13)
 _PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))  # hb + data-parallel/remainder split: profiles/r05_gemm
 
 
 def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-             splitk: int | None = None, pingpong: int | None = None, band: int = 0,
-             stagger: bool | None = None) -> torch.Tensor:
+             splitk: int | None = None, pingpong: int | None = None, band: int = 0) -> torch.Tensor:
     """``out[M, N] (+)= a[K, M]ᵀ @ b[K, N]`` (bf16 in / out, f32 accumulation).  ``band``: XCD band
     height in output-tile rows for the hb modes (0 = the compiled default)."""
     K, M = a.shape
@@ -74,6 +72,5 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
     ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
               M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
-              _MODES[mode] | ((int(band) & 15) << 8) | (8192 if (_STAG if stagger is None else stagger) else 0),
-              _lib.stream_ptr(a.device))
+              _MODES[mode] | ((int(band) & 15) << 8), _lib.stream_ptr(a.device))
     return out
