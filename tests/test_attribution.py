@@ -116,3 +116,20 @@ def test_spawn_records_the_session_in_the_same_round_trip(tmp_path, monkeypatch)
             time.sleep(0.05)
     finally:
         task_nursery.use_transports(None)
+
+
+def test_many_forged_task_ids_do_not_become_many_lookups():
+    """Claims are free to forge: 500 processes each claiming a different unknown task id trigger at
+    most Attestor.MAX_LOOKUPS_PER_S session lookups per second, and the bookkeeping stays bounded."""
+    from tensorhive_fixed_amd.core.attribution import Attestor, SessionRegistry
+
+    calls = []
+    att = Attestor(SessionRegistry(), lookup=lambda host, tid: calls.append(tid), refetch_s=5.0)
+    entry = {"GPU": {"g0": {"processes": [{"pid": 10000 + i, "uid": 1001, "owner": "mallory", "sid": 10000 + i,
+                                            "task_id": str(i)} for i in range(500)]}}}
+    att.attest_entry("node-x", entry)
+    assert len(calls) <= Attestor.MAX_LOOKUPS_PER_S
+    assert all(p["task_id"] is None for p in entry["GPU"]["g0"]["processes"])
+    for i in range(6000):  # warning bookkeeping for many distinct pids stays bounded
+        att.verify("node-x", {"pid": 20000 + i, "uid": 1001, "sid": 1, "task_id": "x"})
+    assert len(att._warned) <= Attestor._MAX_TRACKED
