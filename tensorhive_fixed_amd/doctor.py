@@ -55,6 +55,26 @@ def run_checks() -> list[tuple[str, bool, str]]:
 
     out.append(_check("amdsmi telemetry", smi))
 
+    def hbm_tool():
+        """The in-task HBM counter tool th-run injects: built, the rocprofiler-sdk it resolves at run time
+        present, and no DT_NEEDED on the SDK (a tool that links it makes every task's HIP start ELF-scan
+        all loaded libraries: +3.3 s per task under torch, profiles/r05_daemon/)."""
+        from .core import hbm
+
+        p = hbm.tool_path()
+        if not p:
+            return False, "libthhbm.so not built (HBM bytes fall back to the activity estimate)"
+        sdk = sorted(Path("/opt/rocm/lib").glob("librocprofiler-sdk.so*"))
+        if not sdk:
+            return False, f"{p}: rocprofiler-sdk not installed"
+        if shutil.which("readelf"):
+            dyn = subprocess.run(["readelf", "-d", p], capture_output=True, text=True, timeout=30).stdout
+            if any("(NEEDED)" in ln and "rocprofiler" in ln for ln in dyn.splitlines()):
+                return False, f"{p} links librocprofiler-sdk: every task would start ~3 s later; rebuild it"
+        return True, f"{p} (SDK {sdk[0].name}, resolved at run time)"
+
+    out.append(_check("in-task HBM counter tool (libthhbm)", hbm_tool))
+
     def torch_rocm():
         import torch
 
