@@ -40,10 +40,22 @@ def test_th_run_under_sanitizers(tmp_path, kind):
         argv = tsan_argv(th, *a) if kind == "tsan" else [th, *a]
         return subprocess.run(argv, capture_output=True, text=True, env=env, timeout=timeout)
 
-    r = run("spawn", "--name", "tensorhive_task_a", "--log", str(tmp_path / "a.log"), "--env", "X=1", "--",
-            "bash", "-c", "echo $X; exit 3")
+    # the task-exit datagram path (--notify) runs under the sanitizer too
+    import socket
+
+    ev_path = str(tmp_path / "ev.sock")
+    ev = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
+    ev.bind(ev_path)
+    ev.settimeout(20)
+    r = run("spawn", "--name", "tensorhive_task_a", "--log", str(tmp_path / "a.log"), "--env", "X=1",
+            "--notify", ev_path, "--", "bash", "-c", "echo $X; exit 3")
     assert r.returncode == 0, r.stderr
     assert run("wait", "--name", "tensorhive_task_a", "--timeout", "20").returncode == 3
+    import json as _json
+
+    msg = _json.loads(ev.recv(4096))
+    ev.close()
+    assert msg["event"] == "task_exit" and msg["name"] == "tensorhive_task_a" and msg["exit_code"] == 3
     r = run("spawn", "--name", "tensorhive_task_b", "--log", str(tmp_path / "b.log"), "--", "sleep", "60")
     pid = int(r.stdout.strip())
     ls = run("ls")
