@@ -121,6 +121,7 @@ def main() -> int:
             "zero": 1 if tr.store.sharded else 0,
             "attention": attention_backend(),
             "grad_bucket_mb": args.bucket_mb,
+            "gemm_table": bool(getattr(tr, "gemm_table", False)),  # measured hipBLASLt/rocBLAS choices (ops/tuned)
         },
         "tflops_per_gpu": round(flops / n / 1e12, 1),
         "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,

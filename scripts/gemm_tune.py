@@ -22,7 +22,8 @@ from pathlib import Path
 import torch
 
 ROOT = Path(__file__).resolve().parent.parent
-TUNED = ROOT / "tensorhive_fixed_amd" / "ops" / "tuned" / "gemm_gfx950.csv"
+TUNED = Path(os.environ.get("TH_TUNED_FILE", ROOT / "tensorhive_fixed_amd" / "ops" / "tuned" / "gemm_gfx950.csv"))
+KINDS = set(os.environ.get("TH_TUNE_KINDS", "fwd,dgrad,wgrad").split(","))  # round 5: weight grads run on the TN kernel
 
 T = int(os.environ.get("TH_TUNE_TOKENS", "32768"))  # tokens per micro-step (bench default MB 8 x 4096)
 D, HQKV, FF, V = 4096, 6144, 14336, 128256
@@ -87,6 +88,8 @@ def survey(tag):
     tot_ms, tot_fl = 0.0, 0.0
     rows = []
     for name, kind, M, N, K, res in shapes():
+        if kind not in KINDS:
+            continue
         fn = make(kind, M, N, K, res, dev, name)
         ms = timeit(fn)
         fl = 2.0 * M * N * K
@@ -116,7 +119,8 @@ def main():
         tun.set_max_tuning_iterations(int(os.environ.get("TH_TUNE_ITERS", "20")))
         t0 = time.time()
         survey("tuning-pass")
-        tun.write_file()
+        if hasattr(tun, "write_file"):  # older torch; 2.10 writes the table itself (on exit / per result)
+            tun.write_file()
         print(json.dumps({"tuned_file": str(TUNED), "tuning_s": round(time.time() - t0, 1)}))
         return
     if mode == "check":

@@ -80,6 +80,10 @@ class Trainer:
         self.cfg, self.info = cfg, info
         self.micro_batch, self.seq_len, self.grad_accum = micro_batch, seq_len, grad_accum
         dev = info.device
+        if dev.type == "cuda":
+            from ..ops.tuned import load_gemm_table
+
+            self.gemm_table = load_gemm_table()  # measured hipBLASLt / rocBLAS choices (TH_GEMM_TUNED)
         self.zero = default_zero(info.world) if zero is None else zero
         self.model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
         self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb,
