@@ -186,6 +186,9 @@ class FlatParamStore:
         self.accumulating = False
         self._sync_now = True
         self._ready_seen: set[int] = set()
+        # called with each bucket whose (final micro-batch) gradients are complete and whose
+        # collective, if any, is launched: FlatAdamW's early gradient-norm pass hooks in here
+        self.ready_hook = None
         # exposed-communication spans: bench.py turns them on (TH_COMM_TIMING=1) and reports them
         # per rank; off for training jobs
         self.timer = WaitTimer(self.device, enabled=os.environ.get("TH_COMM_TIMING", "0") == "1")
@@ -248,8 +251,11 @@ class FlatParamStore:
         self._ready_seen.add(key)
         b = self.param_bucket[key]
         b.pending -= 1
-        if b.pending == 0 and self._sync_now and self.collectives:
-            b.handle = self._launch_grad_collective(b)
+        if b.pending == 0 and self._sync_now:
+            if self.collectives:
+                b.handle = self._launch_grad_collective(b)
+            if self.ready_hook is not None:
+                self.ready_hook(b)
 
     def finish_grad_sync(self) -> None:
         """Wait for every bucket; launch any bucket whose params did not all report."""
@@ -333,7 +339,9 @@ class FlatAdamW:
     (23.85k vs 23.81k tokens/s, A/B/A/B on one box): the GEMMs leave the sweep few free CUs.  The next backward
     must not overwrite gradients the sweep still reads: the trainer calls :meth:`wait_done`
     before it (the LM-head gradient, written during the forward, is covered by the head's own
-    bucket wait).
+    bucket wait).  In this mode the clip norm's sums of squares are also taken per bucket during
+    backward (``TH_OPT_SUMSQ_EARLY``, :meth:`_bucket_ready`), so after backward only the sweep
+    itself stands between the last gradient and the next forward's first layer.
     """
 
     def __init__(self, store: FlatParamStore, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
@@ -367,6 +375,18 @@ class FlatAdamW:
         self.exp_avg_sq = torch.zeros_like(self.master)
         self.norm_sq = torch.zeros(1, device=store.device, dtype=torch.float32)
         self.step_count = 0
+        # Early gradient norm (overlapped mode, TH_OPT_SUMSQ_EARLY=1): each bucket's sum of squares
+        # runs on the side stream as soon as the bucket is complete (after its collective), i.e.
+        # during the rest of backward, into its own slot; the step then only sums the slots.
+        # Without it the whole 16 GB gradient is read once more after backward, exposed before
+        # the next forward's first layer can be updated.
+        self.early_sumsq = self.overlap and clip > 0 and os.environ.get("TH_OPT_SUMSQ_EARLY", "1") == "1"
+        self.norm_parts = None
+        self._early_done: set[int] = set()
+        self.early_steps = 0  # steps whose norm came from the early per-bucket sums
+        if self.early_sumsq:
+            self.norm_parts = torch.zeros(len(store.buckets), device=store.device, dtype=torch.float32)
+            store.ready_hook = self._bucket_ready
 
     def step(self, lr: float | None = None) -> None:
         st = self.store
@@ -380,6 +400,24 @@ class FlatAdamW:
                 self.done.record()
         else:
             self._step(lr)
+
+    def _bucket_ready(self, b: _Bucket) -> None:
+        """Store hook: ``||g||^2`` of bucket ``b``'s owned range into ``norm_parts[b.index]``, on the
+        side stream, ordered after the gradient writes (an event on the current stream) and after
+        the bucket's reduce-scatter / all-reduce (``work.wait()`` issued on the side stream)."""
+        st = self.store
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        lo, hi = st.owned_ranges()[b.index]
+        with torch.cuda.stream(self.side):
+            if b.handle is not None:
+                b.handle.wait()
+            if hi > lo:
+                grad_sumsq_(st.grad_buf[lo:hi], self.norm_parts[b.index: b.index + 1])
+            else:
+                self.norm_parts[b.index: b.index + 1].zero_()
+        self._early_done.add(b.index)
 
     def wait_done(self) -> None:
         """Current stream waits for the whole (overlapped) optimizer step."""
@@ -437,7 +475,14 @@ class FlatAdamW:
         st = self.store
         scale = 1.0 / st.world
         groups = self._launch_groups()
-        if self.clip > 0:
+        early = self.early_sumsq and len(self._early_done) == len(st.buckets)
+        self._early_done.clear()
+        if self.clip > 0 and early:
+            self.early_steps += 1
+            torch.sum(self.norm_parts, dim=0, keepdim=True, out=self.norm_sq)
+            if st.sharded and st.collectives:
+                dist.all_reduce(self.norm_sq, op=dist.ReduceOp.SUM, group=st.pg)
+        elif self.clip > 0:
             # ||g||^2 over maximal flat-contiguous runs (the sum does not care about decay groups)
             runs: list[tuple] = []
             merge = os.environ.get("TH_OPT_SUMSQ_RUNS", "1") == "1"  # 0: one pass per segment (old form)
@@ -471,4 +516,6 @@ class FlatAdamW:
 
     def grad_norm(self) -> float:
         """Global gradient norm of the last step (forces a host sync; for logging only)."""
+        if self.done is not None:
+            self.done.synchronize()  # norm_sq is written on the side stream
         return math.sqrt(float(self.norm_sq[0])) / self.store.world

@@ -22,6 +22,32 @@ def test_tiny_llama_overfits_fixed_batch():
     assert losses[-1] < losses[0] - 0.5, losses
 
 
+def test_early_grad_norm_matches_post_backward_norm(monkeypatch):
+    """TH_OPT_SUMSQ_EARLY: the per-bucket sums of squares taken on the side stream during backward
+    give the same clipped steps as the one pass after backward (several buckets, 3 steps)."""
+    from tensorhive_fixed_amd.models.llama3 import LlamaConfig
+    from tensorhive_fixed_amd.parallel.dist import init_distributed
+    from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer
+    info = init_distributed("cuda")
+    runs = {}
+    for early in ("1", "0"):
+        monkeypatch.setenv("TH_OPT_SUMSQ_EARLY", early)
+        tr = Trainer(LlamaConfig.tiny(), info, 2, 128, 1, lr=1e-3, bucket_mb=0.25, seed=3)
+        assert len(tr.store.buckets) > 2
+        norms, losses = [], []
+        for _ in range(3):
+            losses.append(float(tr.step()))
+            norms.append(tr.opt.grad_norm())
+        runs[early] = (norms, losses, tr.opt.early_steps, tr.store.param_buf.float().cpu())
+        del tr
+    (n1, l1, e1, p1), (n0, l0, e0, p0) = runs["1"], runs["0"]
+    assert e1 == 3 and e0 == 0
+    for a, b in zip(n1, n0):
+        assert abs(a - b) <= 1e-5 * b, (n1, n0)
+    assert l1 == pytest.approx(l0, rel=1e-3)
+    assert float((p1 - p0).norm() / p0.norm()) < 1e-3
+
+
 def test_gpu_matches_cpu_reference_loss_and_grads():
     """Same weights on CPU (fp32 reference ops) and GPU (HIP kernels): loss and grads agree."""
     from tensorhive_fixed_amd.models.llama3 import Llama, LlamaConfig

@@ -51,6 +51,24 @@ def test_missing_or_double_gradient_is_an_error():
         store.mark_ready(store.params[0])
 
 
+def test_ready_hook_fires_once_per_bucket_on_the_sync_microbatch_only():
+    """The store's ready hook (FlatAdamW's early gradient-norm pass) sees every bucket exactly once
+    per step, and only when the micro-batch syncs, after all of that bucket's gradients."""
+    m = _model()
+    store = FlatParamStore(m.params_in_backward_order(), torch.device("cpu"), bucket_mb=0.05)
+    seen = []
+    store.ready_hook = lambda b: seen.append((b.index, b.pending))
+    data = SyntheticTokens(CFG.vocab_size, B, S, torch.device("cpu"), 0)
+    for i in range(2):
+        store.begin_microbatch(accumulate=i > 0, sync=i == 1)
+        m(*data.next(), n_valid=2 * B * S).backward()
+        if i == 0:
+            assert seen == []
+    store.finish_grad_sync()
+    assert sorted(i for i, _ in seen) == list(range(len(store.buckets))) and len(store.buckets) > 2
+    assert all(p == 0 for _, p in seen)
+
+
 def _step_on(model, store, opt, batches, world_scale_n):
     for i, (tok, tgt) in enumerate(batches):
         store.begin_microbatch(accumulate=i > 0, sync=i == len(batches) - 1)
