@@ -7,7 +7,7 @@ import time
 
 import torch
 
-os.environ.setdefault("TH_OPT_SUMSQ_EARLY", "1")
+os.environ["TH_OPT_SUMSQ_EARLY"] = "1"  # the form under test (opt-in)
 
 from tensorhive_fixed_amd.models.llama3 import LlamaConfig  # noqa: E402
 from tensorhive_fixed_amd.ops.adamw import grad_sumsq_  # noqa: E402

@@ -339,9 +339,9 @@ class FlatAdamW:
     (23.85k vs 23.81k tokens/s, A/B/A/B on one box): the GEMMs leave the sweep few free CUs.  The next backward
     must not overwrite gradients the sweep still reads: the trainer calls :meth:`wait_done`
     before it (the LM-head gradient, written during the forward, is covered by the head's own
-    bucket wait).  In this mode the clip norm's sums of squares are also taken per bucket during
-    backward (``TH_OPT_SUMSQ_EARLY``, :meth:`_bucket_ready`), so after backward only the sweep
-    itself stands between the last gradient and the next forward's first layer.
+    bucket wait).  With ``TH_OPT_SUMSQ_EARLY=1`` the clip norm's sums of squares are also taken per
+    bucket during backward (:meth:`_bucket_ready`), so after backward only the sweep itself stands
+    between the last gradient and the next forward's first layer.
     """
 
     def __init__(self, store: FlatParamStore, lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
@@ -375,12 +375,12 @@ class FlatAdamW:
         self.exp_avg_sq = torch.zeros_like(self.master)
         self.norm_sq = torch.zeros(1, device=store.device, dtype=torch.float32)
         self.step_count = 0
-        # Early gradient norm (overlapped mode, TH_OPT_SUMSQ_EARLY=1): each bucket's sum of squares
-        # runs on the side stream as soon as the bucket is complete (after its collective), i.e.
-        # during the rest of backward, into its own slot; the step then only sums the slots.
-        # Without it the whole 16 GB gradient is read once more after backward, exposed before
-        # the next forward's first layer can be updated.
-        self.early_sumsq = self.overlap and clip > 0 and os.environ.get("TH_OPT_SUMSQ_EARLY", "1") == "1"
+        # Early gradient norm (overlapped mode, opt-in TH_OPT_SUMSQ_EARLY=1): each bucket's sum of
+        # squares runs on the side stream as soon as the bucket is complete (after its collective),
+        # i.e. during the rest of backward, into its own slot; the step then only sums the slots.
+        # It shortens the exposed optimizer wait (6.2 -> 3.9 ms) but not the one-GPU step, whose
+        # backward has no idle CUs to absorb the sums (profiles/r05_step/README.md), so it is off.
+        self.early_sumsq = self.overlap and clip > 0 and os.environ.get("TH_OPT_SUMSQ_EARLY", "0") == "1"
         self.norm_parts = None
         self._early_done: set[int] = set()
         self.early_steps = 0  # steps whose norm came from the early per-bucket sums
