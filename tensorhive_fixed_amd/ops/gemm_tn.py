@@ -45,10 +45,27 @@ _MODES = {9: 64, 10: 192}
 _PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))  # hb + data-parallel/remainder split: profiles/r05_gemm
 
 
+_BAND_POLICY = os.environ.get("TH_GEMM_TN_BAND_POLICY", "1") == "1"
+
+
+def default_band(m: int, n: int, k: int) -> int:
+    """XCD band height (output-tile rows per band, 1-15; 0 = the compiled default, 8) measured per shape
+    class (profiles/r05_gemm/tn_band2.jsonl, mode 10): the 8-row default is best or within 0.3 % on
+    wqkv / wo / w2; the gate|up gradient (a tall 28672 x 4096 output over K 32768) runs 1.0 % faster in
+    one-row bands, and the LM-head chunk (128256 x 4096 over K 4096) 0.9 % faster in 4-row bands."""
+    if not _BAND_POLICY:
+        return 0
+    if m >= 16384 and n <= 4096 and k >= 16384:
+        return 1
+    if m >= 65536 and k <= 8192:
+        return 4
+    return 0
+
+
 def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-             splitk: int | None = None, pingpong: int | None = None, band: int = 0) -> torch.Tensor:
+             splitk: int | None = None, pingpong: int | None = None, band: int | None = None) -> torch.Tensor:
     """``out[M, N] (+)= a[K, M]ᵀ @ b[K, N]`` (bf16 in / out, f32 accumulation).  ``band``: XCD band
-    height in output-tile rows for the hb modes (0 = the compiled default)."""
+    height in output-tile rows for the hb modes, 0-15 (0 = the compiled default; None = :func:`default_band`)."""
     K, M = a.shape
     K2, N = b.shape
     if K2 != K or tuple(out.shape) != (M, N):
@@ -56,6 +73,8 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
     mode = int(_PP if pingpong is None else pingpong)
     if mode not in _MODES:
         raise ValueError(f"gemm_tn_: launch mode {mode} not in {sorted(_MODES)}")
+    if band is not None and not 0 <= int(band) <= 15:
+        raise ValueError(f"gemm_tn_: band {band} not in 0..15")
     if not a.is_cuda:
         r = a.float().t() @ b.float()
         out.copy_((out.float() + r if accumulate else r).to(out.dtype))
@@ -69,8 +88,10 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
         else:
             torch.mm(a.t(), b, out=out)
         return out
+    if band is None:
+        band = default_band(M, N, K)
     ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
               M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
-              _MODES[mode] | ((int(band) & 15) << 8), _lib.stream_ptr(a.device))
+              _MODES[mode] | (int(band) << 8), _lib.stream_ptr(a.device))
     return out

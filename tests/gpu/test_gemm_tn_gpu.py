@@ -43,7 +43,7 @@ def test_gemm_tn_strided_operands_and_asymmetry(pingpong):
     assert (out.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-2
 
 
-@pytest.mark.parametrize("band", [0, 1, 16])
+@pytest.mark.parametrize("band", [0, 1, 4, 15])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_gemm_tn_data_parallel_plus_remainder_split(accumulate, band):
     """Mode 10: 272 tiles = one data-parallel round of 256 whole tiles + 16 remainder tiles split 2 ways

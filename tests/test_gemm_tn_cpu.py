@@ -51,3 +51,18 @@ def test_retired_launch_modes_are_rejected(mode):
     b = torch.zeros(64, 40, dtype=torch.bfloat16)
     with pytest.raises(ValueError):
         gemm_tn_(a, b, torch.zeros(24, 40, dtype=torch.bfloat16), pingpong=mode)
+
+
+def test_band_policy_and_range():
+    """Per-shape XCD band heights (profiles/r05_gemm/tn_band2.jsonl) and the 4-bit launch field's range."""
+    from tensorhive_fixed_amd.ops import gemm_tn as g
+
+    if g._BAND_POLICY:
+        assert g.default_band(28672, 4096, 32768) == 1  # gate|up weight gradient
+        assert g.default_band(128256, 4096, 4096) == 4  # LM-head chunk
+    for m, n in ((6144, 4096), (4096, 4096), (4096, 14336)):  # wqkv, wo, w2: the compiled default
+        assert g.default_band(m, n, 32768) == 0
+    a, b, out = torch.zeros(64, 256), torch.zeros(64, 256), torch.zeros(256, 256)
+    for bad in (-1, 16):
+        with pytest.raises(ValueError):
+            g.gemm_tn_(a, b, out, band=bad)
