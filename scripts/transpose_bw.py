@@ -27,12 +27,15 @@ def t(fn, it=20):
     return s.elapsed_time(e) / it
 
 
-for R, C in ((32768, 28672), (32768, 4096), (28672, 4096), (4096, 14336), (4096, 6144), (128256, 4096)):
+# the step's weight transposes are [out, in] -> [in, out]: wqkv 6144x4096, wo 4096x4096, w13 28672x4096,
+# w2 4096x14336, LM head 128256x4096
+for R, C in ((32768, 28672), (32768, 4096), (28672, 4096), (4096, 14336), (4096, 6144), (6144, 4096), (4096, 4096),
+             (128256, 4096)):
     x = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
     out = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
     gb = 2 * x.numel() * 2 / 1e9
     res = {"R": R, "C": C}
-    for tile in (0, 2, 3):
+    for tile in (0, 1, 2, 3):
         ms_k = t(lambda: transpose(x, out, tile=tile))
         assert torch.equal(out, x.t())
         res[f"tile{tile}_TBps"] = round(gb / ms_k, 2)
