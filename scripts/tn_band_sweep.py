@@ -24,6 +24,9 @@ def timed(fn, iters=10):
     return statistics.median(ts)
 
 
+BANDS = tuple(int(v) for v in os.environ.get("TN_BANDS", "1,2,4,8,15").split(","))
+
+
 def main():
     _lib.load()
     for name, M, N, T in (("wqkv", 6144, 4096, 32768), ("wo", 4096, 4096, 32768), ("w2", 4096, 14336, 32768),
@@ -35,11 +38,11 @@ def main():
         ref = torch.empty_like(c)
         gemm_tn_(a, b, ref, splitk=sk, pingpong=10, band=0)
         res = {}
-        for band in (1, 2, 4, 8, 15):
+        for band in BANDS:
             gemm_tn_(a, b, c, splitk=sk, pingpong=10, band=band)
             assert ((c.float() - ref.float()).norm() / ref.float().norm()).item() < 1e-3, band  # split order differs
         for _ in range(5):
-            for band in (1, 2, 4, 8, 15):
+            for band in BANDS:
                 res.setdefault(band, []).append(timed(lambda: gemm_tn_(a, b, c, splitk=sk, pingpong=10, band=band)))
         fl = 2.0 * M * N * T
         print(json.dumps({"gemm": name, "K": T, "splitk": sk, **{f"band{k}_ms": round(min(v), 4) for k, v in res.items()},
