@@ -359,7 +359,8 @@ class FlatAdamW:
         # segment indices per bucket, so the sharded step can hand each bucket to its all-gather
         # as soon as its slice is updated
         self.bucket_segments: list[list[int]] = []
-        for lo, hi in store.owned_ranges():
+        self._owned = store.owned_ranges()
+        for lo, hi in self._owned:
             mine = []
             for a, b, wd in ((lo, min(hi, store.decay_numel), weight_decay), (max(lo, store.decay_numel), hi, 0.0)):
                 if b > a:
@@ -409,7 +410,7 @@ class FlatAdamW:
         ev = torch.cuda.Event()
         ev.record()
         self.side.wait_event(ev)
-        lo, hi = st.owned_ranges()[b.index]
+        lo, hi = self._owned[b.index]
         with torch.cuda.stream(self.side):
             if b.handle is not None:
                 b.handle.wait()
