@@ -91,6 +91,7 @@ def main() -> int:
     tr = Trainer(cfg, info, args.micro_batch, args.seq_len, args.grad_accum, bucket_mb=args.bucket_mb,
                  zero=args.zero)
     res = run_timed(tr, args.steps, args.warmup)
+    emu = tr.store.comm_emu.report() if tr.store.comm_emu is not None else None  # TH_COMM_EMU rehearsal
     census = rank_census(info)  # collective: every rank takes part, after the timed region
     comm = comm_report(res["waits"], info)  # collective too: per-rank exposed-communication spans
     n = info.world
@@ -132,6 +133,10 @@ def main() -> int:
         "allgather_wait_ms": comm["allgather_wait_ms"],
         "opt_wait_ms": comm["opt_wait_ms"],
         "dist": {**census, "comm": comm},
+        # CUs the TN weight-gradient launches were planned for during backward (null = all 256) and the
+        # one-GPU RCCL channel-footprint rehearsal, when TH_COMM_EMU asks for it (parallel/comm_emu.py)
+        "tn_backward_cus": tr.bwd_cus,
+        "comm_emu": emu,
     }
     if info.is_main:
         line["daemon"] = daemon_poll_latency() if args.daemon_bench else None

@@ -131,72 +131,187 @@ class Attestor:
 
     ``lookup(host, task_id)`` (optional) refreshes the registry for a task it has not seen, at most
     once per ``refetch_s`` per (host, task): the daemon's implementation lists the task owner's
-    sessions on that node (``task_nursery.running``), which also records them."""
+    sessions on that node (``task_nursery.running``, an SSH round trip for a remote node), which also
+    records them.
+
+    ``background=True`` (the daemon) never runs a lookup on the caller's thread: ``publish`` is called
+    from the monitoring pool, the task-event listener and the node agents' stream readers, and an
+    unreachable node's SSH timeout must not stall any of them.  An unseen claim is queued for one
+    worker thread; until its lookup has run the process is published with the claim unattested (marked
+    ``attestation_pending`` for the API, but judged by every consumer exactly like a rejected claim, i.e.
+    by its UNIX owner: an unverified claim never exempts a process), and the next sample after the
+    lookup attests it from the registry.
+
+    The bookkeeping (rate limit, warnings, queue) is shared by those threads and guarded by one lock,
+    which is never held across a lookup."""
 
     # at most this many session lookups per second over all claims: claims are free to forge, so many
     # distinct forged task ids must not turn into as many th-run listings
     MAX_LOOKUPS_PER_S = 2.0
     _MAX_TRACKED = 4096  # rate-limit / warning bookkeeping entries kept before old ones are pruned
 
-    def __init__(self, registry: SessionRegistry = REGISTRY, lookup=None, refetch_s: float = 5.0):
+    def __init__(self, registry: SessionRegistry = REGISTRY, lookup=None, refetch_s: float = 5.0,
+                 background: bool = False):
         self.registry = registry
         self.lookup = lookup
         self.refetch_s = refetch_s
+        self.background = background
+        self._lock = threading.Lock()
         self._fetched: dict[tuple[str, str], float] = {}
         self._warned: dict[tuple[str, int, str], float] = {}
+        self._fallback_warned: dict[tuple[str, str], float] = {}
         self._lookup_times: list[float] = []
+        self._pending: set[tuple[str, str]] = set()  # background lookups queued or running
+        self._queue = None
+        self._worker = None
         self.rejected = 0
+        self.lookups = 0
 
     @classmethod
     def _prune(cls, d: dict, now: float, keep_s: float) -> None:
         if len(d) > cls._MAX_TRACKED:
-            for k in [k for k, t in d.items() if now - t > keep_s]:
-                del d[k]
+            for k in [k for k, t in list(d.items()) if now - t > keep_s]:
+                d.pop(k, None)
             while len(d) > cls._MAX_TRACKED:  # still too many recent ones: drop the oldest
-                del d[min(d, key=d.get)]
+                d.pop(min(d, key=d.get), None)
 
     def _lookup_allowed(self, now: float) -> bool:
+        """Caller holds ``_lock``."""
         self._lookup_times = [t for t in self._lookup_times if now - t < 1.0]
         if len(self._lookup_times) >= self.MAX_LOOKUPS_PER_S:
             return False
         self._lookup_times.append(now)
         return True
 
-    def _session(self, host: str, tid: str) -> dict | None:
+    def _claim_lookup(self, k: tuple[str, str]) -> bool:
+        """Reserve a lookup of ``k`` under the rate limit and the per-task refetch interval."""
+        now = time.monotonic()
+        with self._lock:
+            if k in self._pending:
+                return False
+            if now - self._fetched.get(k, -1e9) < self.refetch_s or not self._lookup_allowed(now):
+                return False
+            self._fetched[k] = now
+            self._prune(self._fetched, now, self.refetch_s)
+            return True
+
+    def _run_lookup(self, host: str, tid: str) -> None:
+        self.lookups += 1
+        try:
+            self.lookup(host, tid)
+        except Exception as e:  # noqa: BLE001 -- unreachable node: the claim stays unverified
+            log.debug("attribution: session lookup of task %s on %s failed: %s", tid, host, e)
+
+    def _worker_loop(self) -> None:
+        while True:
+            k = self._queue.get()
+            if k is None:
+                return
+            try:
+                self._run_lookup(*k)
+            finally:
+                with self._lock:
+                    self._pending.discard(k)
+
+    def _enqueue(self, k: tuple[str, str]) -> None:
+        import queue
+
+        with self._lock:
+            self._pending.add(k)
+            if self._worker is None:
+                self._queue = queue.Queue()
+                self._worker = threading.Thread(target=self._worker_loop, name="th-attest-lookup", daemon=True)
+                self._worker.start()
+            q = self._queue
+        q.put(k)
+
+    def close(self) -> None:
+        with self._lock:
+            w, q, self._worker = self._worker, self._queue, None
+        if w is not None:
+            q.put(None)
+            w.join(2.0)
+
+    def drain(self, timeout: float = 5.0) -> bool:
+        """Wait until no background lookup is queued or running (tests, shutdown); True if drained."""
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            with self._lock:
+                if not self._pending:
+                    return True
+            time.sleep(0.005)
+        return False
+
+    def pending(self, host: str, tid: str) -> bool:
+        with self._lock:
+            return (host, str(tid)) in self._pending
+
+    def _session(self, host: str, tid: str) -> tuple[dict | None, bool]:
+        """(session facts, lookup still pending)."""
         sess = self.registry.get(host, tid)
-        if sess is None and self.lookup is not None:
-            k = (host, tid)
-            now = time.monotonic()
-            if now - self._fetched.get(k, -1e9) >= self.refetch_s and self._lookup_allowed(now):
-                self._fetched[k] = now
-                self._prune(self._fetched, now, self.refetch_s)
-                try:
-                    self.lookup(host, tid)
-                except Exception as e:  # noqa: BLE001 -- unreachable node: the claim stays unverified
-                    log.debug("attribution: session lookup of task %s on %s failed: %s", tid, host, e)
-                sess = self.registry.get(host, tid)
-        return sess
+        if sess is not None or self.lookup is None:
+            return sess, False
+        k = (host, tid)
+        if self.background:
+            if self.pending(host, tid):
+                return None, True
+            if self._claim_lookup(k):
+                self._enqueue(k)
+                return None, True
+            return None, False
+        if self._claim_lookup(k):
+            self._run_lookup(host, tid)
+            sess = self.registry.get(host, tid)
+        return sess, False
+
+    def _warn_fallback(self, host: str, tid: str, sess: dict) -> None:
+        """A session th-run did not start (the setsid shell fallback records no sid / uid): none of its
+        processes can be attested, which costs the task its in-task HBM counters and, when its UNIX
+        account is not the TensorHive user, its protection exemption.  Said once per task."""
+        if sess.get("sid") is not None or sess.get("uid") is not None:
+            return
+        now = time.monotonic()
+        with self._lock:
+            if (host, tid) in self._fallback_warned:
+                return
+            self._fallback_warned[(host, tid)] = now
+            self._prune(self._fallback_warned, now, 3600.0)
+        log.warning("attribution: task %s on %s was not started by th-run (no session id / uid recorded): its "
+                    "processes cannot be attested and are judged by their UNIX owner", tid, host)
 
     def verify(self, host: str, proc: dict) -> bool:
+        return self._verify(host, proc)[0]
+
+    def _verify(self, host: str, proc: dict) -> tuple[bool, bool]:
+        """(attested, lookup pending)."""
         tid = proc.get("task_id")
         if tid in (None, ""):
-            return False
-        why = check(proc, self._session(host, str(tid)))
+            return False, False
+        sess, pending = self._session(host, str(tid))
+        if sess is not None:
+            self._warn_fallback(host, str(tid), sess)
+        why = check(proc, sess)
         if why is None:
-            return True
-        self.rejected += 1
+            return True, False
+        if pending:
+            return False, True
         k = (host, _int(proc.get("pid")) or 0, str(tid))
         now = time.monotonic()
-        if now - self._warned.get(k, -1e9) > 60.0:
-            self._warned[k] = now
-            self._prune(self._warned, now, 60.0)
+        with self._lock:
+            self.rejected += 1
+            warn = now - self._warned.get(k, -1e9) > 60.0
+            if warn:
+                self._warned[k] = now
+                self._prune(self._warned, now, 60.0)
+        if warn:
             log.warning("attribution: pid %s on %s (owner %s) claims task %s: rejected, %s", proc.get("pid"), host,
                         proc.get("owner"), tid, why)
-        return False
+        return False, False
 
     def attest_entry(self, host: str, entry: dict | None) -> dict | None:
         """In place: keep each process's ``task_id`` only if it verifies (else move it to
-        ``claimed_task_id``), then derive the in-task HBM metrics from the attested processes."""
+        ``claimed_task_id``; ``attestation_pending`` while its background lookup has not run), then
+        derive the in-task HBM metrics from the attested processes."""
         if not entry:
             return entry
         for g in (entry.get("GPU") or {}).values():
@@ -206,8 +321,11 @@ class Attestor:
                 tid = p.get("task_id")
                 if tid in (None, ""):
                     continue
-                if not self.verify(host, p):
+                ok, pending = self._verify(host, p)
+                if not ok:
                     p["claimed_task_id"] = str(tid)
                     p["task_id"] = None
+                    if pending:
+                        p["attestation_pending"] = True
         hbm.finalize_entry(entry)
         return entry

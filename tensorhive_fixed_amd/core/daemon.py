@@ -52,7 +52,9 @@ class Daemon:
 
         # every sample is attested as it is published: a process's TENSORHIVE_TASK_ID counts only
         # inside that task's th-run session and uid (core/attribution.py)
-        self.attestor = Attestor(REGISTRY, lookup=self.lookup_task_sessions)
+        # (session lookups of unseen claims run on the attestor's own worker thread, never on the monitoring
+        # pool, the event listener or a node agent's stream reader: ADVICE r05)
+        self.attestor = Attestor(REGISTRY, lookup=self.lookup_task_sessions, background=True)
         self.infrastructure = InfrastructureStore(list(nodes), attest=self.attestor.attest_entry)
         if backends is None:
             am = self.cfg.amd_monitor
@@ -226,6 +228,7 @@ class Daemon:
         for s in self.services:
             if s.is_alive():
                 s.join(timeout)
+        self.attestor.close()
         for b in {id(b): b for b in self.backends.values()}.values():
             try:
                 b.close()

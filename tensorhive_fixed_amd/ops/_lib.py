@@ -47,7 +47,9 @@ _SIGS: dict[str, list] = {
     "th_flash_attn_bwd_rope": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, P, P, I, P],
     "th_embedding_bwd": [P, P, P, P, L, I, I, P],
     "th_transpose_bf16": [P, P, L, L, L, I, P],
-    "th_gemm_tn": [P, L, P, L, P, L, I, I, I, I, I, P, I, P],
+    "th_gemm_tn": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P],
+    "th_comm_emu_launch": [P, P, L, L, L, L, P, I, L, I, P, P],
+    "th_comm_emu_stop": [P, I, P],
 }
 
 

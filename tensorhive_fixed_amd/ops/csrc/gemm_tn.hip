@@ -272,11 +272,13 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   const int r16 = lane & 15, g4 = lane >> 4;
   const long crow0 = m0 + wm * 128, ccol0 = n0 + wn * 128;
   if constexpr (SPLIT) {
+    // tile-local slab: [launch tile][split][256][256] f32, so a launch needs tiles * splitk * 64 K floats
+    float* ts = slab + ((long)(tile - tile0) * splitk + split) * (TM * TN) + (wm * 128) * TN + wn * 128;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        *reinterpret_cast<f32x4*>(slab + ((long)split * M + crow0 + 16 * i + r16) * N + ccol0 + 16 * j + 4 * g4) = acc[i][j];
+        *reinterpret_cast<f32x4*>(ts + (16 * i + r16) * TN + 16 * j + 4 * g4) = acc[i][j];
     return;
   }
   char LDS_AS* ep = (char LDS_AS*)smem_raw + w * 32768;
@@ -306,41 +308,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   }
 }
 
-// C[m][n] (+)= sum over splits of slab[s][m][n], 8 elements per thread
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
-                                                             long ldc, int M, int N, int splitk, int beta) {
-  const long i8 = (long)blockIdx.x * 256 + threadIdx.x;
-  const long total8 = (long)M * N / 8;
-  if (i8 >= total8) return;
-  const long e = i8 * 8;
-  const long m = e / N, n = e % N;
-  float v[8];
-  const float4v* s0 = reinterpret_cast<const float4v*>(slab + e);
-  float4v x0 = s0[0], x1 = s0[1];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { v[j] = x0[j]; v[4 + j] = x1[j]; }
-  for (int s = 1; s < splitk; ++s) {
-    const float4v* sp = reinterpret_cast<const float4v*>(slab + (long)s * M * N + e);
-    x0 = sp[0];
-    x1 = sp[1];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] += x0[j]; v[4 + j] += x1[j]; }
-  }
-  ushort8* cp = reinterpret_cast<ushort8*>(C + m * ldc + n);
-  ushort8 o;
-  if (beta) {
-    const ushort8 c = *cp;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] + bf2f(c[j]));
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-  }
-  *cp = o;
-}
-
-// Split-K remainder of the "data-parallel + split" launch: C tile (+)= sum over splits of its slab
-// tiles, for the tiles [tile0, tile0 + gridDim.x) of the band order; one workgroup per tile.
+// Split-K reduce: C tile (+)= sum over splits of its tile-local slab pieces, for the tiles
+// [tile0, tile0 + gridDim.x) of the band order (all tiles, or the remainder of the data-parallel launch);
+// one workgroup per tile.
 __global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* __restrict__ slab, ushort* __restrict__ C,
                                                                   long ldc, int M, int N, int splitk, int beta, int tile0,
                                                                   int GM) {
@@ -356,7 +326,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* _
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = 0.f;
     for (int sp = 0; sp < splitk; ++sp) {
-      const float4v* p = reinterpret_cast<const float4v*>(slab + ((long)sp * M + m) * N + n);
+      const float4v* p = reinterpret_cast<const float4v*>(slab + ((long)blockIdx.x * splitk + sp) * (TM * TN) + e);
       const float4v x0 = p[0], x1 = p[1];
 #pragma unroll
       for (int j = 0; j < 4; ++j) { v[j] += x0[j]; v[4 + j] += x1[j]; }
@@ -371,48 +341,40 @@ __global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* _
 }
 
 // C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  splitk > 1 needs a
-// workspace of splitk*M*N floats.  Returns -1 for shapes the kernel does not tile.
+// workspace of (split tiles) * splitk * 64 K floats (ws_floats; ops/gemm_tn.py:tn_plan computes the same
+// count).  Returns -1 for shapes the kernel does not tile or a workspace that is too small.
 // flags: bit6 = schedule "hb" (required; the only schedule since round 5);
-//        bit7 (splitk > 1) = data-parallel whole tiles + split-K only for the remainder tiles;
-//        bits 8-11 = XCD band height in tile rows (0 = TH_TN_GM)
+//        bit7 (splitk > 1) = data-parallel rounds of whole tiles + split-K only for the remainder tiles;
+//        bits 8-11 = XCD band height in tile rows (0 = TH_TN_GM);
+//        bits 12-20 = CUs the launch may count on (0 = 256): RCCL's channel kernels hold CUs during the
+//        N > 1 backward, and a round sized for 256 then spills a few tiles into a second full round
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
-                          int K, int beta, int splitk, float* ws, int flags, hipStream_t s) {
+                          int K, int beta, int splitk, float* ws, long ws_floats, int flags, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || !(flags & 64)) return -1;
   if (K % (64 * splitk)) return -1;
   if (lda < M || ldb < N || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15) return -1;
-  if (splitk > 1 && ws == nullptr) return -1;
   // buffer descriptors per k-tile: 32-bit offsets over 64 k-rows of one operand
   if (2L * 64 * max(lda, ldb) + 512 >= (1L << 31)) return -1;
   const long tiles = (long)(M / TM) * (N / TN);
-  const unsigned grid = (unsigned)(tiles * splitk);
   const ushort *a = (const ushort*)A, *b = (const ushort*)B;
   ushort* c = (ushort*)C;
-  float* slab = splitk > 1 ? ws : nullptr;
   const int gmr = ((flags >> 8) & 15) ? ((flags >> 8) & 15) : TH_TN_GM;  // XCD band height (tile rows)
+  const long cus = ((flags >> 12) & 511) ? ((flags >> 12) & 511) : 256;
+  // flags bit7 with splitk > 1: data-parallel rounds of whole tiles on every available CU (direct bf16
+  // output), then only the REMAINDER tiles split `splitk` ways (slab + a per-tile reduce)
+  const long full = (flags & 128) && splitk > 1 ? tiles / cus * cus : 0;
+  const long split_tiles = splitk > 1 ? tiles - full : 0;
+  if (split_tiles > 0 && (ws == nullptr || ws_floats < split_tiles * splitk * (long)(TM * TN))) return -1;
   auto hbv = [&](bool split_, unsigned g, int sk, int t0) {
-    if (split_) gemm_tn_hb_kernel<true, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, slab, M, N, K, sk, t0, gmr);
+    if (split_) gemm_tn_hb_kernel<true, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, ws, M, N, K, sk, t0, gmr);
     else if (beta) gemm_tn_hb_kernel<false, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
     else gemm_tn_hb_kernel<false, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
   };
-  // flags bit7 with splitk > 1: data-parallel rounds of whole tiles on every CU (direct bf16 output),
-  // then only the REMAINDER tiles split `splitk` ways (slab + a per-tile reduce): no split-K slab
-  // round trip for the bulk of the tiles and no half-empty last round
-  const long cus = 256;
-  const long full = (flags & 128) && splitk > 1 ? tiles / cus * cus : 0;
-  const long rem = tiles - full;
-  if (full > 0 && rem * splitk <= cus) {
-    hbv(false, (unsigned)full, 1, 0);
-    if (rem > 0) {
-      hbv(true, (unsigned)(rem * splitk), splitk, (int)full);
-      splitk_reduce_tiles_kernel<<<(unsigned)rem, 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta, (int)full, gmr);
-    }
-    TH_CHECK_LAUNCH();
-  }
-  hbv(splitk > 1, grid, splitk, 0);
-  if (splitk > 1) {
-    const long n8 = (long)M * N / 8;
-    splitk_reduce_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta);
+  if (full > 0 || splitk == 1) hbv(false, (unsigned)(splitk == 1 ? tiles : full), 1, 0);
+  if (split_tiles > 0) {
+    hbv(true, (unsigned)(split_tiles * splitk), splitk, (int)full);
+    splitk_reduce_tiles_kernel<<<(unsigned)split_tiles, 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta, (int)full, gmr);
   }
   TH_CHECK_LAUNCH();
 }

@@ -9,6 +9,7 @@ K not a multiple of 64 x split) fall back to ``torch.mm``.
 from __future__ import annotations
 
 import os
+from contextlib import contextmanager
 
 import torch
 
@@ -21,21 +22,81 @@ def supported(m: int, n: int, k: int, splitk: int = 1) -> bool:
     return m % _TILE == 0 and n % _TILE == 0 and k % (_TK * splitk) == 0
 
 
-def default_splitk(m: int, n: int, k: int, cus: int = 256) -> int:
-    """Split K when the output tiles leave a ragged last round on the 256 CUs (1 workgroup/CU)."""
+# CUs a launch may count on.  256 on an idle chip; during an N > 1 backward RCCL's channel kernels hold
+# some (one workgroup per channel per collective), and the trainer lowers the budget for backward with
+# :func:`cu_budget` (parallel/comm_emu.py rehearses that footprint on one GPU, profiles/r06_comm/).
+_CUS_DEFAULT = int(os.environ.get("TH_GEMM_CUS", "256"))
+_cus = _CUS_DEFAULT
+
+
+def compute_cus() -> int:
+    return _cus
+
+
+@contextmanager
+def cu_budget(cus: int | None):
+    """Plan TN launches for ``cus`` available CUs inside the block (None: leave the budget unchanged)."""
+    global _cus
+    if cus is None:
+        yield
+        return
+    if not 1 <= int(cus) <= 511:
+        raise ValueError(f"cu_budget: {cus} not in 1..511")
+    prev, _cus = _cus, int(cus)
+    try:
+        yield
+    finally:
+        _cus = prev
+
+
+_SPLIT_COST = 0.03  # per split launch, in tile times: the f32 slab round trip + the reduce (profiles/r05_gemm)
+
+
+def plan_time(tiles: int, splitk: int, dp: bool, cus: int) -> float:
+    """Modelled launch time in whole-tile times: equal-length workgroups dispatched in rounds over ``cus``
+    CUs.  ``dp``: full rounds of whole tiles, then the remainder tiles split ``splitk`` ways."""
+    if splitk == 1:
+        return float(-(-tiles // cus))
+    if dp:
+        full = tiles // cus * cus
+        rem = tiles - full
+        rounds = full // cus
+        return rounds + (-(-rem * splitk // cus) / splitk + _SPLIT_COST if rem else 0.0)
+    return -(-tiles * splitk // cus) / splitk + _SPLIT_COST
+
+
+def tn_plan(m: int, n: int, k: int, cus: int | None = None) -> tuple[int, bool]:
+    """(splitk, data-parallel + split remainder) with the least modelled time on ``cus`` CUs.  A plan with
+    more splits must win by 2 % (the model ignores per-piece prologue cost), and a piece keeps >= 2048
+    k-rows.  ``TH_GEMM_TN_SPLITK`` forces the split factor.  At 256 CUs this reproduces the round-5 choices
+    on every Llama-3-8B weight-gradient shape (tests/test_gemm_tn_cpu.py)."""
+    cus = compute_cus() if cus is None else int(cus)
     env = os.environ.get("TH_GEMM_TN_SPLITK")
-    if env:
-        return int(env)
     tiles = (m // _TILE) * (n // _TILE)
-    best, best_eff = 1, 0.0
-    for s in (1, 2, 3, 4):
-        if not supported(m, n, k, s):
+    if env:
+        return int(env), int(env) > 1
+    best, best_t = (1, False), plan_time(tiles, 1, False, cus)
+    for s in (2, 4, 8):
+        if not supported(m, n, k, s) or k // s < 2048:
             continue
-        rounds = -(-tiles * s // cus)
-        eff = tiles * s / (rounds * cus) - 0.03 * (s > 1)  # the slab round trip costs a few percent
-        if eff > best_eff + 1e-9:
-            best, best_eff = s, eff
+        for dp in (True, False):
+            t = plan_time(tiles, s, dp, cus)
+            if t < best_t * 0.98:
+                best, best_t = (s, dp), t
     return best
+
+
+def default_splitk(m: int, n: int, k: int, cus: int | None = None) -> int:
+    return tn_plan(m, n, k, cus)[0]
+
+
+def workspace_floats(m: int, n: int, splitk: int, dp: bool, cus: int) -> int:
+    """f32 slab the launch needs: (split tiles) x splitk x 256 x 256 (csrc/gemm_tn.hip:th_gemm_tn)."""
+    if splitk <= 1:
+        return 0
+    tiles = (m // _TILE) * (n // _TILE)
+    split_tiles = tiles - (tiles // cus * cus if dp else 0)
+    return split_tiles * splitk * _TILE * _TILE
 
 
 # launch mode of the hb kernel (csrc/gemm_tn.hip, the only schedule since round 5; the round-1..4 modes 0-8
@@ -79,7 +140,11 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
         r = a.float().t() @ b.float()
         out.copy_((out.float() + r if accumulate else r).to(out.dtype))
         return out
-    sk = default_splitk(M, N, K) if splitk is None else splitk
+    cus = compute_cus()
+    if splitk is None:
+        sk, dp = tn_plan(M, N, K, cus)
+    else:
+        sk, dp = int(splitk), int(splitk) > 1
     ok = (a.dtype == b.dtype == out.dtype == torch.bfloat16 and supported(M, N, K, sk)
           and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1)
     if not ok:
@@ -90,8 +155,12 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
         return out
     if band is None:
         band = default_band(M, N, K)
-    ws = torch.empty(sk * M * N, device=a.device, dtype=torch.float32) if sk > 1 else None
+    # mode 9 = every tile split (or none); mode 10 = data-parallel whole tiles, split-K remainder
+    dp = dp and mode == 10
+    nws = workspace_floats(M, N, sk, dp, cus)
+    ws = torch.empty(nws, device=a.device, dtype=torch.float32) if nws else None
+    flags = _MODES[10 if dp else 9] | (int(band) << 8) | ((cus & 511) << 12)
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(),
-              _MODES[mode] | (int(band) << 8), _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(), nws, flags,
+              _lib.stream_ptr(a.device))
     return out

@@ -1,0 +1,143 @@
+"""One-GPU rehearsal of the CUs RCCL's channel kernels take from the N > 1 step (``ops/csrc/comm_emu.hip``).
+
+On 8 ranks every gradient bucket's reduce-scatter runs as one RCCL kernel with one workgroup per channel,
+concurrently with the rest of backward, and each channel workgroup holds its CU for the whole collective.
+A one-rank process group issues the same calls but its collectives are near no-ops, so the one-GPU
+rehearsals of rounds 1-5 never saw that contention (round-5 verdict, weak #1).  This module puts it back:
+
+* ``TH_COMM_EMU="cus=32"`` (persist mode, the stress case): from the first bucket-ready point of a step
+  until ``finish_grad_sync``, ``cus`` channel workgroups (one per CU) stream HBM on a high-priority side
+  stream.  A launch is bounded by ``slice_ms`` and re-issued at every bucket-ready point, so the channels
+  cover the whole backward; the stop marker is written on the compute stream at ``finish_grad_sync``
+  (stream-ordered after backward's last kernel) and ends every queued launch.
+* ``TH_COMM_EMU="cus=16,mode=bucket,world=8,busbw=300"`` (the modelled 8-rank step): one launch per
+  bucket, queued in bucket order on the side stream like RCCL's own stream, each lasting the ring
+  reduce-scatter time of that bucket, ``bytes * (world - 1) / world / busbw``.
+
+``copy`` (GB/s, all channels together; 0 = unthrottled) sets the HBM share: a ring step reads the local
+slice and the peer's incoming slice and lands the peer's writes, about 3 bytes of HBM traffic per byte of
+bus bandwidth, so the default 450 GB/s of copy (= 900 GB/s of HBM reads + writes) models ~300 GB/s of
+bus bandwidth.  One channel workgroup streams at most a few tens of GB/s, so small ``cus`` counts reach
+less than the target (the stats show what was moved).
+
+The emulator only occupies CUs and HBM; it moves no gradient data (the one-rank collectives still run
+and keep the numerics exact).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+
+from ..ops import _lib
+
+_CHUNK_VEC = 4096  # float4 per workgroup per iteration (64 KB)
+
+
+@dataclass
+class EmuConfig:
+    cus: int = 0                # channel workgroups = CUs held while a launch is resident
+    mode: str = "persist"       # persist | bucket
+    world: int = 8              # bucket mode: modelled ranks
+    busbw: float = 300.0        # bucket mode: modelled ring bus bandwidth, GB/s
+    copy: float = 450.0         # HBM copy rate of all channels together, GB/s (0 = unthrottled)
+    slice_ms: float = 50.0      # hard time limit of one launch
+    buffer_mb: float = 512.0    # per direction; larger than the 256 MB MALL so the copy reaches HBM
+
+    def __post_init__(self):
+        if not 0 <= self.cus <= 128:
+            raise ValueError(f"comm emulation: cus {self.cus} not in 0..128")
+        if self.mode not in ("persist", "bucket"):
+            raise ValueError(f"comm emulation: mode {self.mode!r} (persist | bucket)")
+        if self.world < 2 or self.busbw <= 0 or self.copy < 0 or self.slice_ms <= 0:
+            raise ValueError("comm emulation: world >= 2, busbw > 0, copy >= 0, slice_ms > 0")
+
+    def bucket_seconds(self, nbytes: int) -> float:
+        """Ring reduce-scatter time of one bucket of ``nbytes`` at the modelled bus bandwidth."""
+        return nbytes * (self.world - 1) / self.world / (self.busbw * 1e9)
+
+
+def parse(spec: str | None) -> EmuConfig | None:
+    """``"cus=32,mode=persist,copy=450"`` -> :class:`EmuConfig` (None for an empty spec or cus=0)."""
+    if not spec:
+        return None
+    kw: dict = {}
+    types = {"cus": int, "world": int, "mode": str, "busbw": float, "copy": float, "slice_ms": float,
+             "buffer_mb": float}
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        k, _, v = part.partition("=")
+        if k not in types or not v:
+            raise ValueError(f"TH_COMM_EMU: bad field {part!r} (fields: {', '.join(types)})")
+        kw[k] = types[k](v)
+    cfg = EmuConfig(**kw)
+    return cfg if cfg.cus > 0 else None
+
+
+class CommEmulator:
+    """Channel workgroups on a high-priority side stream, driven by the bucket-ready / grad-sync points of
+    :class:`~tensorhive_fixed_amd.parallel.flat.FlatParamStore`."""
+
+    def __init__(self, cfg: EmuConfig, device: torch.device):
+        self.cfg, self.device = cfg, torch.device(device)
+        n = cfg.cus
+        slice_vec = int(cfg.buffer_mb * 2**20 / 16 / n) // _CHUNK_VEC * _CHUNK_VEC
+        self.slice_vec = max(_CHUNK_VEC, slice_vec)
+        self.src = torch.zeros(n * self.slice_vec * 4, device=self.device, dtype=torch.float32)
+        self.dst = torch.empty_like(self.src)
+        self.stop_marker = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self.stats = torch.zeros(4, device=self.device, dtype=torch.int64)
+        self.side = torch.cuda.Stream(device=self.device, priority=-1)
+        self.gen = 1              # the generation of the current step's launches
+        self.active = False       # a launch of this generation was issued
+        self.launches = 0
+        # per-workgroup copy rate -> 100 MHz ticks per 64-KB chunk (0 = unthrottled)
+        per_wg = cfg.copy * 1e9 / n if cfg.copy > 0 else 0.0
+        self.ticks_per_chunk = int(_CHUNK_VEC * 16 / per_wg * 1e8) if per_wg > 0 else 0
+
+    @classmethod
+    def from_env(cls, device: torch.device) -> "CommEmulator | None":
+        cfg = parse(os.environ.get("TH_COMM_EMU"))
+        if cfg is None or torch.device(device).type != "cuda":
+            return None
+        return cls(cfg, device)
+
+    def _launch(self, budget_vec: int, slice_us: int) -> None:
+        _lib.call("th_comm_emu_launch", self.src.data_ptr(), self.dst.data_ptr(), self.slice_vec, _CHUNK_VEC,
+                  budget_vec, self.ticks_per_chunk, self.stop_marker.data_ptr(), self.gen, slice_us, self.cfg.cus,
+                  self.stats.data_ptr(), self.side.cuda_stream)
+        self.launches += 1
+        self.active = True
+
+    def bucket_ready(self, nbytes: int) -> None:
+        """A gradient bucket is complete on the current stream (its collective would start now)."""
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        cfg = self.cfg
+        if cfg.mode == "persist":
+            self._launch(0, int(cfg.slice_ms * 1000))
+            return
+        secs = cfg.bucket_seconds(nbytes)
+        rate = cfg.copy * 1e9 if cfg.copy > 0 else 1e12
+        budget_vec = max(_CHUNK_VEC, int(secs * rate / 16 / cfg.cus) // _CHUNK_VEC * _CHUNK_VEC)
+        self._launch(budget_vec, max(1, int(min(secs * 4, cfg.slice_ms / 1000) * 1e6)))
+
+    def stop(self) -> None:
+        """End of backward (the compute stream): every launch of this step exits."""
+        if not self.active:
+            return
+        _lib.call("th_comm_emu_stop", self.stop_marker.data_ptr(), self.gen, _lib.stream_ptr(self.device))
+        self.gen += 1
+        self.active = False
+
+    def report(self) -> dict:
+        """Totals since construction (one synchronize): launches, workgroups, GB copied, CU-ms resident."""
+        self.side.synchronize()
+        wg, nbytes, ticks, _ = (int(x) for x in self.stats.tolist())
+        return {"spec": os.environ.get("TH_COMM_EMU", ""), "mode": self.cfg.mode, "cus": self.cfg.cus,
+                "launches": self.launches, "workgroups": wg, "copied_gb": round(nbytes / 1e9, 3),
+                "cu_ms_resident": round(ticks / 1e5, 1), "ms_per_workgroup": round(ticks / 1e5 / max(1, wg), 3)}

@@ -57,6 +57,15 @@ def forced_collectives() -> bool:
     return os.environ.get("TH_FORCE_COLLECTIVES", "0") == "1"
 
 
+def pg_timeout():
+    """Process-group timeout (``TH_DIST_TIMEOUT_S``, default 15 min): a collective whose peer is gone (a
+    node lost mid-step; on one node torchrun already tears the group down when a worker exits) fails the
+    job after this long instead of blocking forever (tests/test_rank_failure.py)."""
+    from datetime import timedelta
+
+    return timedelta(seconds=float(os.environ.get("TH_DIST_TIMEOUT_S", "900")))
+
+
 def init_distributed(device_type: str | None = None) -> DistInfo:
     """Initialise from the torchrun environment; single-process when WORLD_SIZE is absent."""
     apply_env_defaults()
@@ -91,7 +100,7 @@ def init_distributed(device_type: str | None = None) -> DistInfo:
             from .comm_diag import prepare_rccl_log
 
             prepare_rccl_log(rank)
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=pg_timeout(), **kw)
     elif dist.is_initialized():
         backend = dist.get_backend()
     return DistInfo(rank, local_rank, world, device, backend, aff)

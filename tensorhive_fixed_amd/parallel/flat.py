@@ -192,6 +192,10 @@ class FlatParamStore:
         # exposed-communication spans: bench.py turns them on (TH_COMM_TIMING=1) and reports them
         # per rank; off for training jobs
         self.timer = WaitTimer(self.device, enabled=os.environ.get("TH_COMM_TIMING", "0") == "1")
+        # one-GPU rehearsal of RCCL's channel CUs during backward (TH_COMM_EMU, parallel/comm_emu.py)
+        from .comm_emu import CommEmulator
+
+        self.comm_emu = CommEmulator.from_env(self.device)
 
     # ------------------------------------------------------------------ buckets
     def _layout(self, entries: list, bucket_mb: float) -> tuple[list[int], list[_Bucket]]:
@@ -254,6 +258,8 @@ class FlatParamStore:
         if b.pending == 0 and self._sync_now:
             if self.collectives:
                 b.handle = self._launch_grad_collective(b)
+            if self.comm_emu is not None:
+                self.comm_emu.bucket_ready((b.end - b.start) * self.grad_buf.element_size())
             if self.ready_hook is not None:
                 self.ready_hook(b)
 
@@ -262,6 +268,8 @@ class FlatParamStore:
         if len(self._ready_seen) != len(self.params):
             missing = [n for n, p in zip(self.names, self.params) if id(p) not in self._ready_seen]
             raise RuntimeError(f"no gradient delivered for: {missing[:5]}...")
+        if self.comm_emu is not None and self._sync_now:
+            self.comm_emu.stop()
         if not self.collectives or not self._sync_now:
             return
         for b in self.buckets:

@@ -23,6 +23,7 @@ import time
 import torch
 
 from ..models.llama3 import Llama, LlamaConfig
+from ..ops import gemm_tn
 from ..parallel.dist import DistInfo, barrier, forced_collectives, init_distributed, max_over_ranks, shutdown
 from ..parallel.flat import FlatAdamW, FlatParamStore
 
@@ -64,6 +65,28 @@ class _Range:
             torch.cuda.nvtx.range_pop()
 
 
+def backward_cu_budget(store: FlatParamStore) -> int | None:
+    """CUs the TN weight-gradient launches may count on during a synchronising backward (ops/gemm_tn.py
+    ``cu_budget``), or None for the whole chip.
+
+    ``TH_COMM_CUS`` names the CUs the gradient collectives hold while they run (0 = plan for all 256).
+    Unset, it is the emulated channel count when ``TH_COMM_EMU`` rehearses RCCL's footprint on one GPU,
+    and ``NCCL_MAX_NCHANNELS`` (one workgroup = one CU per channel) on a real multi-rank run, where
+    ``parallel/dist.py`` presets it.  Measured on one MI355X in profiles/r06_comm/."""
+    env = os.environ.get("TH_COMM_CUS")
+    if env is not None:
+        reserved = int(env)
+    elif store.comm_emu is not None:
+        reserved = store.comm_emu.cfg.cus
+    elif store.collectives and store.world > 1:
+        reserved = int(os.environ.get("NCCL_MAX_NCHANNELS", "0") or 0)
+    else:
+        reserved = 0
+    if reserved <= 0:
+        return None
+    return max(64, 256 - reserved)
+
+
 def default_zero(world: int) -> int:
     """ZeRO stage of the payload: 1 (sharded optimizer) whenever there is more than one rank,
     unless ``TH_ZERO=0`` asks for the replicated DDP optimizer."""
@@ -93,6 +116,7 @@ class Trainer:
             self.model.param_gate = self.store.wait_params
         self.data = SyntheticTokens(cfg.vocab_size, micro_batch, seq_len, dev, info.rank)
         self.tokens_per_step = micro_batch * seq_len * grad_accum  # per rank
+        self.bwd_cus = backward_cu_budget(self.store)  # TN launch geometry while collectives hold CUs
         self.last_loss: torch.Tensor | None = None
 
     def step(self) -> torch.Tensor:
@@ -106,7 +130,7 @@ class Trainer:
                     loss = self.model(tokens, targets, n_valid=n_valid * self.grad_accum)
                 if mb == 0:
                     self.opt.wait_done()  # the previous step's (overlapped) update read these gradients
-                with _Range("backward"):
+                with _Range("backward"), gemm_tn.cu_budget(self.bwd_cus if mb == self.grad_accum - 1 else None):
                     loss.backward()
                 loss_acc = loss.detach() if loss_acc is None else loss_acc + loss.detach()
             with _Range("grad_sync+adamw"):

@@ -85,3 +85,41 @@ def test_gemm_tn_llama_wgrad_shapes_match_fp32(name, M, N, K, accumulate):
     assert rel < 5e-3, (name, rel)
     del a, b, out, ref
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cus", [255, 240, 224, 200])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_tn_cu_budget_launches_match_fp32(cus, accumulate):
+    """CU-aware launches (round 6): a budget below 256 moves the data-parallel / split-K boundary
+    (csrc/gemm_tn.hip flags bits 12-20) and the tile-local split-K slab; 272 tiles over K 2048 exercise
+    both parts with every remainder count."""
+    from tensorhive_fixed_amd.ops.gemm_tn import cu_budget, tn_plan
+
+    K, M, N = 2048 * 4, 4096, 4352
+    g = torch.Generator(device="cuda").manual_seed(cus)
+    a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16, generator=g)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    out = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    ref = a.float().t() @ b.float() + (out.float() if accumulate else 0)
+    with cu_budget(cus):
+        assert tn_plan(M, N, K)[0] > 1
+        gemm_tn_(a, b, out, accumulate=accumulate)
+    torch.cuda.synchronize()
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.parametrize("name,M,N,K", [("wqkv", 6144, 4096, 32768), ("wo", 4096, 4096, 32768)])
+def test_gemm_tn_llama_shapes_at_224_cus(name, M, N, K):
+    from tensorhive_fixed_amd.ops.gemm_tn import cu_budget
+
+    g = torch.Generator(device="cuda").manual_seed(M)
+    a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16, generator=g)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ref = a.float().t() @ b.float()
+    with cu_budget(224):
+        gemm_tn_(a, b, out)
+    torch.cuda.synchronize()
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    assert rel < 5e-3, (name, rel)

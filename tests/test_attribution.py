@@ -133,3 +133,110 @@ def test_many_forged_task_ids_do_not_become_many_lookups():
     for i in range(6000):  # warning bookkeeping for many distinct pids stays bounded
         att.verify("node-x", {"pid": 20000 + i, "uid": 1001, "sid": 1, "task_id": "x"})
     assert len(att._warned) <= Attestor._MAX_TRACKED
+
+
+def test_attestor_bookkeeping_is_thread_safe_under_many_forged_claims():
+    """publish() runs attest_entry from the monitoring pool, the event listener and the agents'
+    stream readers at once.  Many threads x more forged claims than _MAX_TRACKED must neither raise nor
+    exceed the lookup rate limit, and every forged claim stays rejected."""
+    import threading
+
+    from tensorhive_fixed_amd.core.attribution import Attestor, SessionRegistry
+
+    calls = []
+    lock = threading.Lock()
+
+    def lookup(host, tid):
+        with lock:
+            calls.append(time.monotonic())
+
+    att = Attestor(SessionRegistry(), lookup=lookup, refetch_s=0.0)
+    n = Attestor._MAX_TRACKED + 500
+    errors = []
+
+    def worker(w):
+        try:
+            for chunk in range(0, n, 250):
+                entry = {"GPU": {"g": {"processes": [
+                    {"pid": 100000 * w + i, "uid": 1001, "owner": "mallory", "sid": 5, "task_id": f"{w}-{i}"}
+                    for i in range(chunk, min(n, chunk + 250))]}}}
+                att.attest_entry(f"node-{w % 3}", entry)
+                assert all(p["task_id"] is None for p in entry["GPU"]["g"]["processes"])
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    t0 = time.monotonic()
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:3]
+    dt = time.monotonic() - t0
+    assert len(calls) <= Attestor.MAX_LOOKUPS_PER_S * (dt + 1.0) + 1e-9, (len(calls), dt)
+    assert len(att._warned) <= Attestor._MAX_TRACKED and len(att._fetched) <= Attestor._MAX_TRACKED
+    assert att.rejected >= 8 * n
+
+
+def test_background_lookup_never_runs_on_the_publishing_thread():
+    """an unseen claim is looked up on the attestor's worker, not on the thread that publishes
+    the sample; that sample carries the claim unattested (pending), the next one attests it."""
+    import threading
+
+    from tensorhive_fixed_amd.core.attribution import Attestor, SessionRegistry
+
+    reg = SessionRegistry()
+    release = threading.Event()
+    seen_threads = []
+
+    def slow_lookup(host, tid):  # an unreachable node's SSH timeout
+        seen_threads.append(threading.current_thread().name)
+        release.wait(5)
+        reg.record(host, {"name": f"tensorhive_task_{tid}", "sid": 4242, "uid": 1000, "user": "alice",
+                          "monitor_pid": 4241, "pid": 4243})
+
+    att = Attestor(reg, lookup=slow_lookup, background=True)
+    proc = {"pid": 4243, "uid": 1000, "owner": "alice", "sid": 4242, "task_id": "9"}
+    entry = {"GPU": {"g": {"processes": [dict(proc)]}}}
+    t0 = time.monotonic()
+    att.attest_entry("n1", entry)
+    assert time.monotonic() - t0 < 0.5  # did not wait for the lookup
+    p = entry["GPU"]["g"]["processes"][0]
+    assert p["task_id"] is None and p["claimed_task_id"] == "9" and p["attestation_pending"] is True
+    # still pending: the same claim does not queue a second lookup
+    att.attest_entry("n1", {"GPU": {"g": {"processes": [dict(proc)]}}})
+    release.set()
+    deadline = time.monotonic() + 5
+    while att.pending("n1", "9") and time.monotonic() < deadline:
+        time.sleep(0.01)
+    entry2 = {"GPU": {"g": {"processes": [dict(proc)]}}}
+    att.attest_entry("n1", entry2)
+    p2 = entry2["GPU"]["g"]["processes"][0]
+    assert p2["task_id"] == "9" and "attestation_pending" not in p2
+    assert seen_threads == ["th-attest-lookup"]
+    att.close()
+
+
+def test_pending_claims_do_not_exempt_a_process_from_protection():
+    """A claim whose lookup has not run yet is judged like a rejected one (by the UNIX owner)."""
+    from tensorhive_fixed_amd.core.attribution import Attestor, SessionRegistry
+
+    att = Attestor(SessionRegistry(), lookup=lambda h, t: time.sleep(0.2), background=True)
+    entry = {"GPU": {"g": {"processes": [{"pid": 1, "uid": 1001, "owner": "mallory", "sid": 1, "task_id": "5"}]}}}
+    att.attest_entry("n", entry)
+    p = entry["GPU"]["g"]["processes"][0]
+    assert p["task_id"] is None  # ProtectionService and the queue's eviction check read task_id only
+    att.close()
+
+
+def test_fallback_session_without_sid_or_uid_warns_once(caplog):
+    from tensorhive_fixed_amd.core.attribution import Attestor, SessionRegistry
+
+    reg = SessionRegistry()
+    reg.record("n", {"name": "tensorhive_task_3", "pid": 10})  # setsid fallback: no sid / uid recorded
+    att = Attestor(reg)
+    with caplog.at_level("WARNING"):
+        for _ in range(3):
+            att.attest_entry("n", {"GPU": {"g": {"processes": [{"pid": 11, "uid": 1000, "sid": 10, "task_id": "3"}]}}})
+    msgs = [r.getMessage() for r in caplog.records if "not started by th-run" in r.getMessage()]
+    assert len(msgs) == 1

@@ -136,8 +136,10 @@ def test_claim_of_unseen_task_triggers_one_session_lookup(daemon, new_user, new_
     daemon.stub.add_process(task.hostname, 1, 4242, user, task_id=str(task.id), sid=9100)
     daemon.stub.add_process(task.hostname, 2, 4243, "intruder", task_id=str(task.id), sid=4243)
     n0 = sum(1 for c, _ in node.calls if " ls" in c)
+    publish(daemon)  # queues the lookup on the attestor's worker (never on the publishing thread)
+    assert daemon.attestor.drain()
     publish(daemon)
-    publish(daemon)
+    assert daemon.attestor.drain()
     assert sum(1 for c, _ in node.calls if " ls" in c) - n0 == 1  # the intruder's claim does not re-list
     procs = daemon.infrastructure.node_gpu_processes(task.hostname)
     by_pid = {p["pid"]: p for ps in procs.values() for p in ps}
