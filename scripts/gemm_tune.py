@@ -106,6 +106,28 @@ def survey(tag):
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "survey"
     tun = torch.cuda.tunable
+    # TH_TUNE_EMU="cus=16": measure / tune with an emulated RCCL channel kernel holding that many CUs
+    # (parallel/comm_emu.py) -- the table a multi-rank step wants, whose GEMMs share the chip with RCCL
+    emu = None
+    if os.environ.get("TH_TUNE_EMU"):
+        sys.path.insert(0, str(ROOT))
+        from tensorhive_fixed_amd.ops import _lib
+        from tensorhive_fixed_amd.parallel.comm_emu import CommEmulator, parse
+
+        _lib.load()
+        emu = CommEmulator(parse(os.environ["TH_TUNE_EMU"] + ",copy=1,slice_ms=5000,buffer_mb=64"), torch.device("cuda"))
+        emu.hold(float(os.environ.get("TH_TUNE_EMU_S", "1500")))
+        torch.cuda.synchronize()
+    try:
+        _run(mode, tun)
+    finally:
+        if emu is not None:
+            emu.stop()
+            torch.cuda.synchronize()
+            emu.side.synchronize()
+
+
+def _run(mode, tun):
     if mode in ("tune", "resume"):
         TUNED.parent.mkdir(parents=True, exist_ok=True)
         if mode == "tune" and TUNED.exists():

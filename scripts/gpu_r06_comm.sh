@@ -17,12 +17,14 @@ if [ "${PART:-1}" = "1" ]; then
     grep -o '"value": [0-9.]*' $O/k${k}_fix.log
   done
 else
-  # VARIANTS: name=TH_COMM_EMU spec (empty = no emulation); names ending in _nofix plan TN for 256 CUs
+  # VARIANTS: "name|TH_COMM_EMU spec|VAR=val;VAR=val" (spec empty = no emulation; names ending in _nofix plan
+  # TN for 256 CUs)
   cd /tmp && export TMPDIR=/tmp
-  for v in ${VARIANTS:-base= k8_nofix=cus=8}; do
-    name=${v%%=*}; spec=${v#*=}
+  for v in ${VARIANTS:-"base||" "k8_nofix|cus=8|"}; do
+    IFS='|' read -r name spec envs <<< "$v"
     case $name in *_nofix) export TH_COMM_CUS=0;; *) unset TH_COMM_CUS;; esac
-    TH_COMM_EMU="$spec" timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$name -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --daemon-bench 0 > $R/$O/prof_$name.log 2>&1 || exit 1
+    ( IFS=';'; for e in $envs; do [ -n "$e" ] && export "$e"; done
+      TH_COMM_EMU="$spec" timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$name -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --daemon-bench 0 > $R/$O/prof_$name.log 2>&1 ) || exit 1
     python3 $R/scripts/step_summary.py $(ls $R/$O/prof_$name/*kernel_stats.csv | head -1) --steps 4 > $R/$O/step_summary_$name.txt 2>&1; head -18 $R/$O/step_summary_$name.txt
   done
 fi

@@ -87,7 +87,8 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--hbm-glob", default=None, help="counter files to merge (default /dev/shm/th-hbm-*.json)")
     ap.add_argument("--events", default=None, metavar="SOCK",
                     help="unix datagram socket th-run notifies on task exit (core/events.py): the agent "
-                         "samples the node at once and forwards the event")
+                         "samples the node at once and forwards the event.  'auto': a socket in a fresh "
+                         "private directory; the bound path is reported as the stream's first line")
     args = ap.parse_args(argv)
 
     stop = {"flag": False}
@@ -99,12 +100,15 @@ def main(argv: list[str] | None = None) -> int:
         signal.signal(sig, _stop)
     backend = build_backend(args)
     period = max(0.02, args.stream / 1000.0) if args.stream > 0 else 0.0
-    ev_sock = None
+    ev_sock = ev_path = ev_tmp = None
     if args.events and period > 0:
         from .core.events import open_event_socket
 
         try:
-            ev_sock, _path, _tmp = open_event_socket(args.events)
+            ev_sock, ev_path, ev_tmp = open_event_socket(args.events)
+            # the daemon hands th-run --notify only the path an agent reports having bound (a
+            # fixed world-writable path can be squatted by another local user)
+            print(json.dumps({"v": 1, "host": args.host, "events_socket": ev_path}), flush=True)
         except OSError as e:  # another agent's socket, a squatted path: exits are found by polling
             print(json.dumps({"v": 1, "warning": f"task events unavailable: {e}"[:300]}), flush=True)
     rc = 0
@@ -159,7 +163,9 @@ def main(argv: list[str] | None = None) -> int:
         if ev_sock is not None:
             try:
                 ev_sock.close()
-                os.unlink(args.events)
+                os.unlink(ev_path)
+                if ev_tmp:
+                    os.rmdir(ev_tmp)
             except OSError:
                 pass
         try:

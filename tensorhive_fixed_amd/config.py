@@ -330,9 +330,10 @@ class LauncherConfig:
     # daemon's own node always uses this install's copy
     hbm_tool: str = ""
     # task exits as events (core/events.py): th-run notifies the daemon (its own node) or the node
-    # agent (remote nodes, on this socket path of the node) when a task has ended
+    # agent (remote nodes) when a task has ended; "auto" = the agent binds a private socket and reports
+    # its path (a fixed path in /tmp could be squatted by another local user)
     task_events: bool = True
-    node_events_socket: str = "/tmp/tensorhive-agent-events.sock"
+    node_events_socket: str = "auto"
 
 
 @dataclass
@@ -506,7 +507,7 @@ def load_config(directory: Path | str | None = None) -> Config:
             rccl_proto=main.str("launcher", "rccl_proto", ""),
             hbm_tool=main.str("launcher", "hbm_tool", ""),
             task_events=main.bool("launcher", "task_events", True),
-            node_events_socket=main.str("launcher", "node_events_socket", "/tmp/tensorhive-agent-events.sock"),
+            node_events_socket=main.str("launcher", "node_events_socket", "auto"),
         ),
     )
 

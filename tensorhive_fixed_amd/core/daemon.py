@@ -122,7 +122,7 @@ class Daemon:
             return self.events.path if self.events is not None else None
         b = self.backends.get(host)
         if isinstance(b, RemoteBackend) and b.node_mode(host) == "agent" and b.stream_ms:
-            return self.cfg.launcher.node_events_socket or None
+            return b.event_socket(host)  # only a path the node's agent reported having bound
         return None
 
     # a host is re-sampled for task events at most this often: the node socket takes datagrams from any

@@ -41,12 +41,15 @@ def parse_event(data: bytes) -> dict | None:
 
 
 def open_event_socket(path: str | None = None) -> tuple[socket.socket, str, str | None]:
-    """A bound unix datagram socket any local user may send to.  Without ``path`` it lives in a
-    fresh private directory (returned third, to remove on close); with ``path`` an existing
-    socket file of ours is replaced, anything else is refused."""
+    """A bound unix datagram socket any local user may send to.  Without ``path`` (or ``"auto"``) it
+    lives in a fresh private directory under ``$XDG_RUNTIME_DIR`` or the temp dir (mode 0711: nobody
+    can pre-create or replace the socket; returned third, to remove on close); with ``path`` an
+    existing socket file of ours is replaced, anything else is refused."""
     tmpdir = None
-    if path is None:
-        tmpdir = tempfile.mkdtemp(prefix="tensorhive-events-")
+    if path in (None, "", "auto"):
+        base = os.environ.get("XDG_RUNTIME_DIR")
+        base = base if base and os.path.isdir(base) and os.access(base, os.W_OK) else None
+        tmpdir = tempfile.mkdtemp(prefix="tensorhive-events-", dir=base)
         os.chmod(tmpdir, 0o711)  # others may reach the socket by its name, not list the directory
         path = os.path.join(tmpdir, "events.sock")
     else:

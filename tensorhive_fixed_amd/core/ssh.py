@@ -108,25 +108,83 @@ def authorized_keys_entry(key_path: Path | str, host: str | None = None) -> str:
     return f"{parts[0]} {parts[1]} tensorhive@{host or socket.gethostname()}"
 
 
-def verify_login_as(host: str, username: str, key_path: str) -> bool:
-    """Self-signup proof: can TensorHive's key log into ``host`` as ``username``?"""
-    spec = get_config().ssh.available_nodes.get(host, {})
-    if spec.get("transport") == "local":
-        import pwd
+def _ssh_login_ok(host: str, username: str, port: int, key_path: str) -> bool:
+    """The reference's proof (``tensorhive/controllers/user.py:99-117``): log into ``host`` AS
+    ``username`` with TensorHive's key and run ``true``."""
+    t = SSHTransport(host, username, int(port), key_path, get_config().ssh.proxy, get_config().ssh.timeout)
+    try:
+        return t.run("true", timeout=get_config().ssh.timeout + 5).ok
+    except Exception:  # noqa: BLE001 -- no sshd / no route: not a proof
+        return False
 
+
+def authorized_keys_lists_key(username: str, key_path: str) -> tuple[bool, str]:
+    """Fallback proof on the daemon's own node: ``username``'s ``~/.ssh/authorized_keys`` lists
+    TensorHive's public key as a key entry.  Trusted only when sshd itself would trust the file
+    (``StrictModes``): ``~/.ssh`` and the file are owned by that user, are not group- or
+    world-writable and are not symlinks; the home directory is not group- or world-writable either.
+    Returns (proved, reason)."""
+    import pwd
+    import stat as st
+
+    try:
+        pw = pwd.getpwnam(username)
+    except KeyError:
+        return False, "no such user on this node"
+    try:
+        key = public_key(key_path).split()
+        ktype, kdata = key[0], key[1]
+    except (OSError, subprocess.CalledProcessError, IndexError):
+        return False, "TensorHive's key is unreadable"
+    home = Path(pw.pw_dir)
+    sshdir, ak = home / ".ssh", home / ".ssh" / "authorized_keys"
+    for p, what in ((home, "home directory"), (sshdir, "~/.ssh"), (ak, "authorized_keys")):
         try:
-            pwd.getpwnam(username)
-        except KeyError:
-            return False
-        ak = Path(pwd.getpwnam(username).pw_dir) / ".ssh" / "authorized_keys"
-        try:
-            key = public_key(key_path).split()[1]
-            return ak.exists() and key in ak.read_text()
-        except (OSError, subprocess.CalledProcessError, IndexError):
-            return False
-    t = SSHTransport(host, username, int(spec.get("port", 22)), key_path, get_config().ssh.proxy,
-                     get_config().ssh.timeout)
-    return t.run("true", timeout=get_config().ssh.timeout + 5).ok
+            info = os.lstat(p)
+        except OSError:
+            return False, f"{what} is not readable by the daemon"
+        if st.S_ISLNK(info.st_mode):
+            return False, f"{what} is a symlink"
+        if p != home and info.st_uid != pw.pw_uid:
+            return False, f"{what} is not owned by {username}"
+        if p == home and info.st_uid not in (pw.pw_uid, 0):
+            return False, f"{what} is not owned by {username}"
+        if info.st_mode & 0o022:
+            return False, f"{what} is group- or world-writable"
+    try:
+        fd = os.open(ak, os.O_RDONLY | os.O_NOFOLLOW)
+        with os.fdopen(fd, "r", errors="replace") as f:
+            text = f.read(1 << 20)
+    except OSError:
+        return False, "authorized_keys is not readable by the daemon"
+    for line in text.splitlines():
+        parts = line.strip().split()
+        if not parts or parts[0].startswith("#"):
+            continue
+        # options may precede the key type: find "<type> <base64>" as consecutive fields
+        for i in range(len(parts) - 1):
+            if parts[i] == ktype and parts[i + 1] == kdata:
+                return True, "key listed"
+    return False, "TensorHive's key is not listed"
+
+
+def verify_login_as(host: str, username: str, key_path: str) -> bool:
+    """Self-signup proof: can TensorHive's key log into ``host`` as ``username``?
+
+    Remote nodes: an SSH login as the user, as in the reference.  The daemon's own node
+    (``transport = local``): the same SSH login to the node first; only when that cannot be made
+    (no sshd on the node) the user's ``authorized_keys``, read with sshd's own ownership and mode
+    rules (:func:`authorized_keys_lists_key`) -- a non-root daemon that cannot read it gets no proof."""
+    spec = get_config().ssh.available_nodes.get(host, {})
+    port = int(spec.get("port", 22))
+    if spec.get("transport") == "local":
+        if _ssh_login_ok(spec.get("address") or "localhost", username, port, key_path):
+            return True
+        ok, why = authorized_keys_lists_key(username, key_path)
+        if not ok:
+            log.info("sign-up proof for %s on %s failed: %s", username, host, why)
+        return ok
+    return _ssh_login_ok(host, username, port, key_path)
 
 
 def node_tty_sessions(transport: Transport) -> list[dict]:

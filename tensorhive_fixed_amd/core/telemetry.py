@@ -412,6 +412,12 @@ class RemoteBackend(TelemetryBackend):
         self.errors: dict[str, str] = {}
         self._lock = threading.Lock()
         self.on_event = None  # (host, event) -> None: task exits the node agent forwards (core/events.py)
+        self._event_sockets: dict[str, str] = {}  # host -> task-exit socket the running agent reported binding
+
+    def event_socket(self, host: str) -> str | None:
+        """The task-exit socket the node's current agent bound (None until it reported one)."""
+        with self._lock:
+            return self._event_sockets.get(host)
 
     def node_mode(self, host: str) -> str:
         return self._modes.get(host, self.mode)
@@ -441,6 +447,8 @@ class RemoteBackend(TelemetryBackend):
                     log.warning("node agent unavailable on %s (%s); falling back to th-smi", host,
                                 self.errors.get(host, "no output"))
                     self._modes[host] = "th-smi"
+        with self._lock:
+            self._event_sockets.pop(host, None)  # a new agent binds (and reports) its own socket
         p = subprocess.Popen(self._argv(host), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, bufsize=1)
         self._procs[host] = p
         self._started[host] = time.time()
@@ -456,6 +464,11 @@ class RemoteBackend(TelemetryBackend):
                 if mode == "agent":
                     if doc.get("error"):
                         self.errors[host] = doc["error"]
+                        continue
+                    if isinstance(doc.get("events_socket"), str):
+                        with self._lock:
+                            if self._procs.get(host) is p:
+                                self._event_sockets[host] = doc["events_socket"]
                         continue
                     if doc.get("event") is not None:  # a task on the node exited (after a fresh entry)
                         cb = self.on_event

@@ -47,7 +47,7 @@ _SIGS: dict[str, list] = {
     "th_flash_attn_bwd_rope": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, L, L, L, L, F, P, P, I, P],
     "th_embedding_bwd": [P, P, P, P, L, I, I, P],
     "th_transpose_bf16": [P, P, L, L, L, I, P],
-    "th_gemm_tn": [P, L, P, L, P, L, I, I, I, I, I, P, L, I, P],
+    "th_gemm_tn": [P, L, P, L, P, L, I, I, I, I, I, I, P, L, I, P],
     "th_comm_emu_launch": [P, P, L, L, L, L, P, I, L, I, P, P],
     "th_comm_emu_stop": [P, I, P],
 }
@@ -73,6 +73,17 @@ def load(build_if_missing: bool = False) -> C.CDLL:
             raise RuntimeError(
                 f"gfx950 kernel library {_LIB_PATH} is missing: run "
                 "`python -m tensorhive_fixed_amd.ops.build` (no eager fallback on GPU)")
+        if "TH_KERNEL_LIB" not in os.environ:
+            # a library built from other sources has other entry-point signatures: ctypes would pass
+            # arguments the C side reads as different ones, so refuse it instead of launching anything
+            from . import build as _build
+
+            if _build.stamp_exists() and not _build.is_up_to_date():
+                if build_if_missing:
+                    _build.build()
+                else:
+                    raise RuntimeError(f"{_LIB_PATH} was built from different sources than ops/csrc: rebuild "
+                                       "with `python -m tensorhive_fixed_amd.ops.build`")
         lib = C.CDLL(str(_LIB_PATH))
         for name, argtypes in _SIGS.items():
             fn = getattr(lib, name, None)

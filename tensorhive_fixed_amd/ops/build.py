@@ -45,6 +45,10 @@ def _stamp_path() -> Path:
     return BUILD_DIR / "libthk.stamp"
 
 
+def stamp_exists() -> bool:
+    return _stamp_path().exists()
+
+
 def is_up_to_date() -> bool:
     return LIB.exists() and _stamp_path().exists() and _stamp_path().read_text().strip() == _digest()
 

@@ -1604,17 +1604,19 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   int var = flags >= 16 ? (flags & 15) : TH_FA_FWD_DEFAULT;
   bool spread = flags >= 16 ? ((flags >> 5) & 1) : TH_FA_FWD_SPREAD;
   if ((long)S * ld * 2 >= (1L << 31)) var &= ~4;  // DMA staging uses 32-bit row offsets
+#define TH_FWD(P, Dd, Db, Km)                                                                      \
+  fa_fwd_kernel<P, Dd, Db, Km><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,  \
+                                                             (const ushort*)v, (ushort*)o, lse, B,  \
+                                                             S, Hq, Hkv, ld, bs, ldo, bso,          \
+                                                             scale * LOG2E, causal)
+#ifdef TH_FA_DIAG
+  // experiment matrix (diagnostic library only: scripts/build_variant_lib.sh fa_diag -DTH_FA_DIAG=1)
   if (var == 15 && spread) {
     fa_fwd_kernel<true, true, true, true, true><<<(unsigned)nblk, 256, 0, s>>>(
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (ushort*)o, lse, B, S, Hq, Hkv, ld, bs, ldo, bso,
         scale * LOG2E, causal);
     TH_CHECK_LAUNCH();
   }
-#define TH_FWD(P, Dd, Db, Km)                                                                      \
-  fa_fwd_kernel<P, Dd, Db, Km><<<(unsigned)nblk, 256, 0, s>>>((const ushort*)q, (const ushort*)k,  \
-                                                             (const ushort*)v, (ushort*)o, lse, B,  \
-                                                             S, Hq, Hkv, ld, bs, ldo, bso,          \
-                                                             scale * LOG2E, causal)
   switch (var) {
     case 0: TH_FWD(false, false, false, false); break;
     case 1: TH_FWD(true, false, false, false); break;
@@ -1629,6 +1631,13 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
     case 15: TH_FWD(true, true, true, true); break;
     default: TH_FWD(true, true, true, true); break;
   }
+#else
+  // production: the default (15: PRESCALE + DEFER + LDS-DMA DBUF + KVMAJOR) and, when the DMA staging's
+  // 32-bit row offsets would overflow, the same kernel with register-staged tiles (11)
+  if (spread || (var != 15 && var != 11)) return -3;
+  if (var == 15) TH_FWD(true, true, true, true);
+  else TH_FWD(true, true, false, true);
+#endif
 #undef TH_FWD
   TH_CHECK_LAUNCH();
 }
@@ -1638,11 +1647,34 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 // kf variant: flags bits 6-18
 static int kf_var_of(int flags) { return (flags >> 6) & 8191; }
 static bool kf_variant_known(int v) {
-  return v == 0 || v == 111 || v == 3439 || v == 7535
+  return v == 7535
+#ifdef TH_FA_DIAG
+         || v == 0 || v == 111 || v == 3439  // earlier kf variants (profiles/r04_flash)
+#endif
 #ifdef TH_KF_DIAG
          || v == 3567 || v == 7663  // s_memtime-stamped builds (diagnostic library only)
 #endif
       ;
+}
+
+// The launch flags the production library serves (ops/attention.py): the default kf path (bit4, kf 7535,
+// bit19), the paired kh kernel (bit19; also the automatic fallback for S % 64 != 0), the fused
+// register-staged dK|dV kernel with the DMA dQ kernel (bit3 + bit19), and register-staged tiles throughout
+// (bit5; also the automatic fallback when 32-bit DMA offsets overflow).  The q-major dQ order, the dQ kernel
+// without the spread DMA, the old dK/dV block order / priority bits and the earlier kf variants exist only in
+// the diagnostic build (-DTH_FA_DIAG).
+static bool flags_shipped(int flags) {
+#ifdef TH_FA_DIAG
+  (void)flags;
+  return true;
+#else
+  const int known = 8 | 16 | 32 | (8191 << 6) | (1 << 19);
+  if (flags & ~known) return false;
+  if (flags & 32) return !(flags & 16);
+  if (!((flags >> 19) & 1)) return false;
+  if (flags & 16) return !(flags & 8) && kf_variant_known(kf_var_of(flags));
+  return kf_var_of(flags) == 0;
+#endif
 }
 
 static int flash_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
@@ -1653,6 +1685,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   if (rcos != nullptr && ((flags & (8 | 32)) || (long)S * ld * 2 >= (1L << 31) || rsin == nullptr))
     return -3;
   if ((flags & 16) && !kf_variant_known(kf_var_of(flags))) return -3;  // before any launch
+  if (!flags_shipped(flags)) return -3;
   if ((flags & 16) && S % C_BQ != 0) flags &= ~16;  // kf assumes whole 64-query tiles: kh instead
   const long nq = (long)((S + F_BM - 1) / F_BM) * Hq * B;
   // flags bit0: q-major block order for the dQ kernel (default: KV-major, see q_block_map);
@@ -1673,6 +1706,7 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
                                                                (const ushort*)dout, (const ushort*)o, lse, delta,     \
                                                                (ushort*)dq, B, S, Hq, Hkv, ld, bs, ldo, bso, scale,   \
                                                                scale * LOG2E, causal, rcos, rsin)
+#ifdef TH_FA_DIAG
   if (flags & 1) {
     if (dq_dma) {
       if (dq_spread) TH_DQ_LAUNCH(false, true, true); else TH_DQ_LAUNCH(false, true, false);
@@ -1686,6 +1720,10 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
       TH_DQ_LAUNCH(true, false, false);
     }
   }
+#else
+  if (dq_dma) TH_DQ_LAUNCH(true, true, true);  // flags_shipped: bit19 is set on every DMA path
+  else TH_DQ_LAUNCH(true, false, false);
+#endif
 #undef TH_DQ_LAUNCH
   }
   // bit4 (ops/attention.py's default, with a kf variant in bits 6-12): the one-wave-per-SIMD kf
@@ -1704,9 +1742,11 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
     // the instantiated variants (profiles/r04_flash/README.md has the measured ones; others are
     // rejected up front by kf_variant_known)
     switch (kvar) {
+#ifdef TH_FA_DIAG
       case 0: TH_KF_LAUNCH(0); break;
       case 111: TH_KF_LAUNCH(111); break;    // bits 0-3, 5, 6
       case 3439: TH_KF_LAUNCH(3439); break;  // 111 + bits 8, 10, 11
+#endif
       case 7535: TH_KF_LAUNCH(7535); break;  // 3439 + -lse2 from the dQ kernel (bit12; the default, attention.py)
 #ifdef TH_KF_DIAG
       case 3567: TH_KF_LAUNCH(3567); break;  // 3439 + s_memtime stamps (th_kf_stamps)
@@ -1729,15 +1769,19 @@ static int flash_bwd_impl(const void* q, const void* k, const void* v, const voi
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)fa_bwd_dkv_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, B_LDS);
+#ifdef TH_FA_DIAG
     (void)hipFuncSetAttribute((const void*)fa_bwd_dkv_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, B_LDS);
+#endif
     attr_set = true;
   }
+#ifdef TH_FA_DIAG
   // flags bit1: the old (kv-block-major) order for dK/dV (default: KV-head-major)
   if (flags & 2)
     fa_bwd_dkv_kernel<false><<<(unsigned)nk, B_THREADS, B_LDS, s>>>(
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
         (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, !(flags & 4));
   else
+#endif
     fa_bwd_dkv_kernel<true><<<(unsigned)nk, B_THREADS, B_LDS, s>>>(
         (const ushort*)q, (const ushort*)k, (const ushort*)v, (const ushort*)dout, lse, delta, (ushort*)dk,
         (ushort*)dv, B, S, Hq, Hkv, ld, bs, ldo, bso, scale, scale * LOG2E, causal, !(flags & 4));

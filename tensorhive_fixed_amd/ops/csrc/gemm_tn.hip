@@ -86,19 +86,28 @@ constexpr bool kTnDiag = false;
 //              | 44 barrier;  52- 87 DMA B of tile t+2 (8 pieces, every 5th MFMA)
 //       MFMA  64-127  k-step 1 (Y); 88: vmcnt(16) + barrier (tile t+1 landed); 90-121 read X of tile t+1
 //   * epilogue: bf16 through LDS with 16-B row stores (beta: C added), or f32x4 stores into the split-K slab.
-template <bool SPLIT, bool BETA>
+//   * one grid holds both kinds of workgroup (round 6): the first `full` workgroups are whole-K tiles
+//     0 .. full-1, the rest are `splitk` K-pieces of each remaining tile (into the slab; a reduce follows).
+//     The dispatcher starts workgroups in grid order, so on an idle chip the pieces fill the CUs the whole
+//     tiles leave free, and with CUs held by RCCL's channels the pieces still trail one short round --
+//     instead of the whole-tile round spilling a few tiles into a second full round.  Each part gets its
+//     own XCD remap, so consecutive tiles of a part share an XCD's L2.
+template <bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const ushort* __restrict__ A, long lda, const ushort* __restrict__ B, long ldb,
-    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int tile0,
+    ushort* __restrict__ C, long ldc, float* __restrict__ slab, int M, int N, int K, int splitk, int full,
     int GM) {
   constexpr int HIMG = 64 * ROWB;     // 32 KB: 64 k-rows x 256 columns
   constexpr int HSTAGE = 2 * HIMG;    // A | B
   __shared__ __attribute__((aligned(1024))) char smem_raw[2 * HSTAGE];
   const char LDS_AS* smem = (const char LDS_AS*)smem_raw;
   const int nM = M / TM, nN = N / TN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = tile0 + (SPLIT ? L / splitk : L);
-  const int split = SPLIT ? L % splitk : 0;
+  const int bid = blockIdx.x;
+  const bool is_piece = bid >= full;  // uniform per workgroup
+  const int L = is_piece ? xcd_remap(bid - full, (int)gridDim.x - full) : xcd_remap(bid, full);
+  const int sk = is_piece ? splitk : 1;
+  const int tile = is_piece ? full + L / splitk : L;
+  const int split = is_piece ? L % splitk : 0;
   // GM: output-tile rows per XCD band (runtime: launch flags bits 8-11, default TH_TN_GM)
   const int per_band = GM * nN;
   const int band = tile / per_band;
@@ -108,7 +117,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   const int tm = first_m + in_band % gm;
   const int tn = in_band / gm;
   const long m0 = (long)tm * TM, n0 = (long)tn * TN;
-  const int kper = K / splitk;
+  const int kper = K / sk;
   const long kbeg = (long)split * kper;
   const int nt = kper / 64;
 
@@ -271,9 +280,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   // lane holds C[m = 16 i + r16][n = 16 j + 4 g4 .. +3] of the wave tile
   const int r16 = lane & 15, g4 = lane >> 4;
   const long crow0 = m0 + wm * 128, ccol0 = n0 + wn * 128;
-  if constexpr (SPLIT) {
-    // tile-local slab: [launch tile][split][256][256] f32, so a launch needs tiles * splitk * 64 K floats
-    float* ts = slab + ((long)(tile - tile0) * splitk + split) * (TM * TN) + (wm * 128) * TN + wn * 128;
+  if (is_piece) {
+    // tile-local slab: [split tile][split][256][256] f32, so a launch needs split tiles * splitk * 64 K floats
+    float* ts = slab + ((long)(tile - full) * splitk + split) * (TM * TN) + (wm * 128) * TN + wn * 128;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -340,16 +349,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_tiles_kernel(const float* _
   }
 }
 
-// C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  splitk > 1 needs a
-// workspace of (split tiles) * splitk * 64 K floats (ws_floats; ops/gemm_tn.py:tn_plan computes the same
-// count).  Returns -1 for shapes the kernel does not tile or a workspace that is too small.
+// C[M][N] (+)= A[K][M]^T B[K][N]; A row stride lda, B ldb, C ldc (elements).  One launch: the first
+// `full` tiles (band order) whole-K, the remaining tiles split `splitk` ways into the f32 workspace
+// (ws_floats >= (tiles - full) * splitk * 64 K; ops/gemm_tn.py:tn_plan picks full / splitk for the CUs the
+// launch may meet), then one reduce workgroup per split tile.  Returns -1 for shapes the kernel does not
+// tile or a workspace that is too small.
 // flags: bit6 = schedule "hb" (required; the only schedule since round 5);
-//        bit7 (splitk > 1) = data-parallel rounds of whole tiles + split-K only for the remainder tiles;
-//        bits 8-11 = XCD band height in tile rows (0 = TH_TN_GM);
-//        bits 12-20 = CUs the launch may count on (0 = 256): RCCL's channel kernels hold CUs during the
-//        N > 1 backward, and a round sized for 256 then spills a few tiles into a second full round
+//        bits 8-11 = XCD band height in tile rows (0 = TH_TN_GM)
 extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N,
-                          int K, int beta, int splitk, float* ws, long ws_floats, int flags, hipStream_t s) {
+                          int K, int beta, int splitk, int full, float* ws, long ws_floats, int flags,
+                          hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || splitk < 1 || !(flags & 64)) return -1;
   if (K % (64 * splitk)) return -1;
   if (lda < M || ldb < N || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return -1;
@@ -357,25 +366,20 @@ extern "C" int th_gemm_tn(const void* A, long lda, const void* B, long ldb, void
   // buffer descriptors per k-tile: 32-bit offsets over 64 k-rows of one operand
   if (2L * 64 * max(lda, ldb) + 512 >= (1L << 31)) return -1;
   const long tiles = (long)(M / TM) * (N / TN);
-  const ushort *a = (const ushort*)A, *b = (const ushort*)B;
-  ushort* c = (ushort*)C;
-  const int gmr = ((flags >> 8) & 15) ? ((flags >> 8) & 15) : TH_TN_GM;  // XCD band height (tile rows)
-  const long cus = ((flags >> 12) & 511) ? ((flags >> 12) & 511) : 256;
-  // flags bit7 with splitk > 1: data-parallel rounds of whole tiles on every available CU (direct bf16
-  // output), then only the REMAINDER tiles split `splitk` ways (slab + a per-tile reduce)
-  const long full = (flags & 128) && splitk > 1 ? tiles / cus * cus : 0;
-  const long split_tiles = splitk > 1 ? tiles - full : 0;
+  if (full < 0 || full > tiles || (splitk == 1 && full != tiles)) return -1;
+  const long split_tiles = tiles - full;
   if (split_tiles > 0 && (ws == nullptr || ws_floats < split_tiles * splitk * (long)(TM * TN))) return -1;
-  auto hbv = [&](bool split_, unsigned g, int sk, int t0) {
-    if (split_) gemm_tn_hb_kernel<true, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, ws, M, N, K, sk, t0, gmr);
-    else if (beta) gemm_tn_hb_kernel<false, true><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
-    else gemm_tn_hb_kernel<false, false><<<g, 256, 0, s>>>(a, lda, b, ldb, c, ldc, nullptr, M, N, K, 1, t0, gmr);
-  };
-  if (full > 0 || splitk == 1) hbv(false, (unsigned)(splitk == 1 ? tiles : full), 1, 0);
-  if (split_tiles > 0) {
-    hbv(true, (unsigned)(split_tiles * splitk), splitk, (int)full);
-    splitk_reduce_tiles_kernel<<<(unsigned)split_tiles, 256, 0, s>>>(ws, c, ldc, M, N, splitk, beta, (int)full, gmr);
-  }
+  const int gmr = ((flags >> 8) & 15) ? ((flags >> 8) & 15) : TH_TN_GM;  // XCD band height (tile rows)
+  const unsigned grid = (unsigned)(full + split_tiles * splitk);
+  if (beta)  // whole tiles add C in their epilogue; the pieces never read C (the reduce adds it)
+    gemm_tn_hb_kernel<true><<<grid, 256, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, ws,
+                                                 M, N, K, splitk, full, gmr);
+  else
+    gemm_tn_hb_kernel<false><<<grid, 256, 0, s>>>((const ushort*)A, lda, (const ushort*)B, ldb, (ushort*)C, ldc, ws,
+                                                  M, N, K, splitk, full, gmr);
+  if (split_tiles > 0)
+    splitk_reduce_tiles_kernel<<<(unsigned)split_tiles, 256, 0, s>>>(ws, (ushort*)C, ldc, M, N, splitk, beta, full,
+                                                                     gmr);
   TH_CHECK_LAUNCH();
 }
 

@@ -49,40 +49,65 @@ def cu_budget(cus: int | None):
         _cus = prev
 
 
-_SPLIT_COST = 0.03  # per split launch, in tile times: the f32 slab round trip + the reduce (profiles/r05_gemm)
+_PIECE_COST = 0.01   # per split-K piece, in whole-tile times: its prologue and the f32 slab write
+_REDUCE_COST = 0.02  # the per-tile reduce kernel after a launch with split tiles
+_CHIP_CUS = 256
 
 
-def plan_time(tiles: int, splitk: int, dp: bool, cus: int) -> float:
-    """Modelled launch time in whole-tile times: equal-length workgroups dispatched in rounds over ``cus``
-    CUs.  ``dp``: full rounds of whole tiles, then the remainder tiles split ``splitk`` ways."""
-    if splitk == 1:
-        return float(-(-tiles // cus))
-    if dp:
-        full = tiles // cus * cus
-        rem = tiles - full
-        rounds = full // cus
-        return rounds + (-(-rem * splitk // cus) / splitk + _SPLIT_COST if rem else 0.0)
-    return -(-tiles * splitk // cus) / splitk + _SPLIT_COST
+def plan_time(tiles: int, splitk: int, full: int, cus: int) -> float:
+    """Modelled time of one launch in whole-tile times: ``full`` whole-K tiles, then ``tiles - full`` tiles
+    split ``splitk`` ways, dispatched in grid order onto ``cus`` CUs, each workgroup to the CU that frees
+    first (csrc/gemm_tn.hip: one grid holds both kinds)."""
+    import heapq
+
+    rem = tiles - full
+    if rem and splitk == 1:
+        full, rem = tiles, 0
+    if cus >= full + rem * splitk:  # everything in one wave
+        t = 1.0 if full else 0.0
+        return max(t, (1.0 / splitk + _PIECE_COST) if rem else 0.0) + (_REDUCE_COST if rem else 0.0)
+    whole_rounds, left = divmod(full, cus)
+    t0 = float(whole_rounds)
+    free = [t0] * (cus - left) + [t0 + 1.0] * left
+    heapq.heapify(free)
+    piece = 1.0 / splitk + _PIECE_COST
+    end = max(free) if left else t0
+    for _ in range(rem * splitk):
+        t = heapq.heappop(free) + piece
+        end = max(end, t)
+        heapq.heappush(free, t)
+    return end + (_REDUCE_COST if rem else 0.0)
 
 
-def tn_plan(m: int, n: int, k: int, cus: int | None = None) -> tuple[int, bool]:
-    """(splitk, data-parallel + split remainder) with the least modelled time on ``cus`` CUs.  A plan with
-    more splits must win by 2 % (the model ignores per-piece prologue cost), and a piece keeps >= 2048
-    k-rows.  ``TH_GEMM_TN_SPLITK`` forces the split factor.  At 256 CUs this reproduces the round-5 choices
-    on every Llama-3-8B weight-gradient shape (tests/test_gemm_tn_cpu.py)."""
-    cus = compute_cus() if cus is None else int(cus)
-    env = os.environ.get("TH_GEMM_TN_SPLITK")
+def tn_plan(m: int, n: int, k: int, cus: int | None = None) -> tuple[int, int]:
+    """(splitk, whole tiles) of the launch.  ``cus``: the CUs the launch may have to live with (default the
+    :func:`cu_budget`); below 256 the plan weighs its time on ``cus`` CUs (RCCL's channels holding the rest)
+    and on the idle chip equally, each against its ideal ``tiles / CUs``.  A plan with more splits must win by
+    2 % (the model ignores everything but rounds), and a piece keeps >= 2048 k-rows.
+    ``TH_GEMM_TN_SPLITK`` forces the split factor (every tile split).  At 256 CUs this reproduces the round-5
+    choices on every Llama-3-8B weight-gradient shape (tests/test_gemm_tn_cpu.py)."""
+    cmin = compute_cus() if cus is None else int(cus)
     tiles = (m // _TILE) * (n // _TILE)
+    env = os.environ.get("TH_GEMM_TN_SPLITK")
     if env:
-        return int(env), int(env) > 1
-    best, best_t = (1, False), plan_time(tiles, 1, False, cus)
+        s = int(env)
+        return s, (tiles if s == 1 else 0)
+    cs = sorted({cmin, _CHIP_CUS}) if cmin < _CHIP_CUS else [cmin]
+
+    def cost(s: int, full: int) -> float:
+        return sum(plan_time(tiles, s, full, c) / (tiles / c) for c in cs) / len(cs)
+
+    best, best_c = (1, tiles), cost(1, tiles)
     for s in (2, 4, 8):
         if not supported(m, n, k, s) or k // s < 2048:
             continue
-        for dp in (True, False):
-            t = plan_time(tiles, s, dp, cus)
-            if t < best_t * 0.98:
-                best, best_t = (s, dp), t
+        fulls = {0} | {tiles - tiles % c for c in cs} | {max(0, tiles - tiles % c - c) for c in cs}
+        for full in sorted(fulls, reverse=True):
+            if full >= tiles:
+                continue
+            c = cost(s, full)
+            if c < best_c * 0.98:
+                best, best_c = (s, full), c
     return best
 
 
@@ -90,20 +115,19 @@ def default_splitk(m: int, n: int, k: int, cus: int | None = None) -> int:
     return tn_plan(m, n, k, cus)[0]
 
 
-def workspace_floats(m: int, n: int, splitk: int, dp: bool, cus: int) -> int:
+def workspace_floats(m: int, n: int, splitk: int, full: int) -> int:
     """f32 slab the launch needs: (split tiles) x splitk x 256 x 256 (csrc/gemm_tn.hip:th_gemm_tn)."""
     if splitk <= 1:
         return 0
     tiles = (m // _TILE) * (n // _TILE)
-    split_tiles = tiles - (tiles // cus * cus if dp else 0)
-    return split_tiles * splitk * _TILE * _TILE
+    return (tiles - full) * splitk * _TILE * _TILE
 
 
 # launch mode of the hb kernel (csrc/gemm_tn.hip, the only schedule since round 5; the round-1..4 modes 0-8
 # were retired, profiles/r05_gemm/): 9 = whole-K tiles, or split-K for every tile when splitk > 1;
-# 10 = whole tiles data-parallel on every CU, split-K only for the remainder tiles
-_MODES = {9: 64, 10: 192}
-_PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))  # hb + data-parallel/remainder split: profiles/r05_gemm
+# 10 = the planned mix: whole tiles first, split-K pieces of the remaining tiles in the same grid
+_MODES = {9: 64, 10: 64}
+_PP = int(os.environ.get("TH_GEMM_TN_PP", "10"))
 
 
 _BAND_POLICY = os.environ.get("TH_GEMM_TN_BAND_POLICY", "1") == "1"
@@ -140,11 +164,14 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
         r = a.float().t() @ b.float()
         out.copy_((out.float() + r if accumulate else r).to(out.dtype))
         return out
-    cus = compute_cus()
-    if splitk is None:
-        sk, dp = tn_plan(M, N, K, cus)
+    tiles = (M // _TILE) * (N // _TILE)
+    if splitk is None and mode == 10:
+        sk, full = tn_plan(M, N, K)
+    elif splitk is None:
+        sk, full = 1, tiles
     else:
-        sk, dp = int(splitk), int(splitk) > 1
+        sk = int(splitk)
+        full = tiles if sk == 1 else (tn_full_for(M, N, sk) if mode == 10 else 0)
     ok = (a.dtype == b.dtype == out.dtype == torch.bfloat16 and supported(M, N, K, sk)
           and a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1)
     if not ok:
@@ -155,12 +182,16 @@ def gemm_tn_(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bo
         return out
     if band is None:
         band = default_band(M, N, K)
-    # mode 9 = every tile split (or none); mode 10 = data-parallel whole tiles, split-K remainder
-    dp = dp and mode == 10
-    nws = workspace_floats(M, N, sk, dp, cus)
+    nws = workspace_floats(M, N, sk, full)
     ws = torch.empty(nws, device=a.device, dtype=torch.float32) if nws else None
-    flags = _MODES[10 if dp else 9] | (int(band) << 8) | ((cus & 511) << 12)
     _lib.call("th_gemm_tn", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              M, N, K, int(accumulate), sk, None if ws is None else ws.data_ptr(), nws, flags,
-              _lib.stream_ptr(a.device))
+              M, N, K, int(accumulate), sk, full, None if ws is None else ws.data_ptr(), nws,
+              _MODES[mode] | (int(band) << 8), _lib.stream_ptr(a.device))
     return out
+
+
+def tn_full_for(m: int, n: int, splitk: int, cus: int | None = None) -> int:
+    """Whole tiles of a mode-10 launch with a forced split factor: the whole rounds that fit ``cus`` CUs."""
+    c = compute_cus() if cus is None else int(cus)
+    tiles = (m // _TILE) * (n // _TILE)
+    return tiles - tiles % c if splitk > 1 else tiles

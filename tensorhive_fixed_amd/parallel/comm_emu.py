@@ -126,6 +126,13 @@ class CommEmulator:
         budget_vec = max(_CHUNK_VEC, int(secs * rate / 16 / cfg.cus) // _CHUNK_VEC * _CHUNK_VEC)
         self._launch(budget_vec, max(1, int(min(secs * 4, cfg.slice_ms / 1000) * 1e6)))
 
+    def hold(self, seconds: float) -> None:
+        """Hold the channel CUs for about ``seconds`` from now (back-to-back bounded launches) or until
+        :meth:`stop`: contention for benchmarks and tuning runs outside a training step."""
+        per = max(1, int(self.cfg.slice_ms * 1000))
+        for _ in range(max(1, int(seconds * 1e6 / per) + 1)):
+            self._launch(0, per)
+
     def stop(self) -> None:
         """End of backward (the compute stream): every launch of this step exits."""
         if not self.active:

@@ -6,6 +6,14 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+# The launch flags the production library serves (csrc/flash_attn.hip flags_shipped, round 6): the default
+# kf path, the paired kh kernel (also the automatic fallback when S % 64 != 0), the fused register-staged
+# dK|dV kernel beside the DMA dQ kernel, and register-staged tiles throughout (the automatic fallback when
+# 32-bit DMA offsets overflow).  The experiment variants live in the TH_FA_DIAG build only.
+KF_DEFAULT = 16 | (7535 << 6) | (1 << 19)
+PROD_FLAGS = [KF_DEFAULT, 1 << 19, 8 | (1 << 19), 32]
+PROD_IDS = ["kf_default", "kh", "fused_dkv", "regstage"]
+
 
 def _ref(qkv, B, S, Hq, Hkv, D, causal=True):
     from tensorhive_fixed_amd.ops.attention import _split, attention_reference
@@ -13,9 +21,7 @@ def _ref(qkv, B, S, Hq, Hkv, D, causal=True):
     return attention_reference(q, k, v, causal).reshape(B * S, Hq * D)
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 7120, 220112, 744400, 1006544, 32],
-                         ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v111", "kf_v3439", "kf_v3439_dq_spread",
-                              "kf_v7535_dq_spread", "regstage"])
+@pytest.mark.parametrize("bwd_flags", PROD_FLAGS, ids=PROD_IDS)
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 128, 4, 1), (2, 200, 8, 2), (1, 1024, 32, 8), (1, 64, 2, 2), (3, 192, 4, 2)])
 def test_flash_fwd_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -64,9 +70,7 @@ def test_qkv_attention_with_rope_matches_sdpa_path():
     assert rel < 2e-2, rel
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 7120, 220112, 744400, 1006544, 32],
-                         ids=["paired_kh_2wg", "fused_dkv", "kf_one_wave", "kf_v111", "kf_v3439", "kf_v3439_dq_spread",
-                              "kf_v7535_dq_spread", "regstage"])
+@pytest.mark.parametrize("bwd_flags", PROD_FLAGS, ids=PROD_IDS)
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 200, 8, 2), (1, 384, 4, 4), (2, 320, 6, 3)])
 def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
@@ -84,19 +88,20 @@ def test_flash_noncausal_bwd_matches_reference(B, S, Hq, Hkv, bwd_flags):
     assert rel < 2e-2, f"dqkv rel err {rel}"
 
 
-@pytest.mark.parametrize("variant", [0, 11, 15, 31], ids=["plain", "prescale_defer", "dma_dbuf", "dma_spread"])
-def test_flash_fwd_variants_match_reference(variant):
+def test_retired_forward_variants_are_rejected():
+    """Production library: only the default forward (and its register-staged twin for offsets past 2^31)."""
     from tensorhive_fixed_amd.ops.attention import flash_fwd
-    torch.manual_seed(2)
-    B, S, Hq, Hkv, D = 2, 328, 8, 2, 128
+    B, S, Hq, Hkv, D = 1, 128, 4, 2, 128
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
-    o, _ = flash_fwd(qkv, B, S, Hq, Hkv, D, variant=variant)
+    o, _ = flash_fwd(qkv, B, S, Hq, Hkv, D, variant=15)
     ref = _ref(qkv.float(), B, S, Hq, Hkv, D)
     assert (o.float() - ref).abs().max().item() < 2e-2
+    for v in (0, 1, 7, 8, 31):
+        with pytest.raises(RuntimeError, match="bad shape"):
+            flash_fwd(qkv, B, S, Hq, Hkv, D, variant=v)
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 8, 16, 220112, 744400, 1006544],
-                         ids=["kh", "fused_dkv", "kf_one_wave", "kf_v3439", "kf_v3439_dq_spread", "kf_v7535_dq_spread"])
+@pytest.mark.parametrize("bwd_flags", [KF_DEFAULT, 1 << 19], ids=["kf_default", "kh"])
 @pytest.mark.parametrize("S,Hq,Hkv", [(4096, 32, 8), (8192, 8, 2)], ids=["S4096_bench_heads", "S8192_model_max"])
 def test_flash_long_sequences_match_fp32(S, Hq, Hkv, bwd_flags):
     """The training shapes: S = 4096 (the bench) with Llama-3-8B's 32/8 heads, and S = 8192 (the
@@ -131,8 +136,7 @@ def test_flash_long_sequences_match_fp32(S, Hq, Hkv, bwd_flags):
         del x, q, k, v, s, p, og, g
 
 
-@pytest.mark.parametrize("bwd_flags", [0, 16, 220112, 744400, 1006544],
-                         ids=["kh", "kf_one_wave", "kf_v3439", "kf_v3439_dq_spread", "kf_v7535_dq_spread"])
+@pytest.mark.parametrize("bwd_flags", [KF_DEFAULT, 1 << 19], ids=["kf_default", "kh"])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 256, 8, 2), (2, 200, 4, 4), (1, 4096, 32, 8)])
 def test_rotary_backward_in_the_kernels_matches_the_separate_pass(B, S, Hq, Hkv, bwd_flags):
     """The rotary backward folded into the dQ / dK epilogues gives the dqkv of the flash backward
@@ -163,3 +167,14 @@ def test_unknown_kf_variant_is_rejected_before_any_launch():
     o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
     with pytest.raises(RuntimeError, match="bad shape"):
         flash_bwd(torch.randn_like(o), qkv, o, lse, B, S, Hq, Hkv, D, flags=16 | (5 << 6))
+
+
+@pytest.mark.parametrize("flags", [16 | (3439 << 6) | (1 << 19), 16 | (7535 << 6), 0, 1 | (1 << 19), 2 | (1 << 19)],
+                         ids=["kf_v3439", "kf_no_dq_spread", "kh_plain_dq", "q_major_dq", "old_dkv_order"])
+def test_retired_backward_flags_are_rejected(flags):
+    from tensorhive_fixed_amd.ops.attention import flash_bwd, flash_fwd
+    B, S, Hq, Hkv, D = 1, 128, 4, 2, 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
+    with pytest.raises(RuntimeError, match="bad shape"):
+        flash_bwd(torch.randn_like(o), qkv, o, lse, B, S, Hq, Hkv, D, flags=flags)

@@ -90,9 +90,8 @@ def test_gemm_tn_llama_wgrad_shapes_match_fp32(name, M, N, K, accumulate):
 @pytest.mark.parametrize("cus", [255, 240, 224, 200])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_gemm_tn_cu_budget_launches_match_fp32(cus, accumulate):
-    """CU-aware launches (round 6): a budget below 256 moves the data-parallel / split-K boundary
-    (csrc/gemm_tn.hip flags bits 12-20) and the tile-local split-K slab; 272 tiles over K 2048 exercise
-    both parts with every remainder count."""
+    """CU-aware launches (round 6): a budget below 256 moves the whole-tile / split-K boundary of the mixed
+    grid and the tile-local split-K slab; 272 tiles over K 8192 exercise both parts for several remainders."""
     from tensorhive_fixed_amd.ops.gemm_tn import cu_budget, tn_plan
 
     K, M, N = 2048 * 4, 4096, 4352
@@ -102,7 +101,8 @@ def test_gemm_tn_cu_budget_launches_match_fp32(cus, accumulate):
     out = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g)
     ref = a.float().t() @ b.float() + (out.float() if accumulate else 0)
     with cu_budget(cus):
-        assert tn_plan(M, N, K)[0] > 1
+        sk, full = tn_plan(M, N, K)
+        assert sk > 1 and 0 < full < 272
         gemm_tn_(a, b, out, accumulate=accumulate)
     torch.cuda.synchronize()
     err = (out.float() - ref).abs().max().item()

@@ -134,6 +134,8 @@ def test_agent_forwards_exit_events(tmp_path):
                           "--stub-gpus", "1", "--host", "n9", "--events", sock], stdout=subprocess.PIPE, text=True,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     try:
+        bound = json.loads(p.stdout.readline())
+        assert bound["events_socket"] == sock  # reported before the first entry
         first = json.loads(p.stdout.readline())
         assert "entry" in first
         t0 = time.time()
@@ -187,6 +189,7 @@ def test_agent_coalesces_an_event_flood(tmp_path):
                           "--stub-gpus", "1", "--host", "n9", "--events", sock], stdout=subprocess.PIPE, text=True,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     try:
+        assert json.loads(p.stdout.readline())["events_socket"] == sock
         assert "entry" in json.loads(p.stdout.readline())
         t0 = time.time()
         while not os.path.exists(sock) and time.time() - t0 < 10:
@@ -209,3 +212,66 @@ def test_agent_coalesces_an_event_flood(tmp_path):
     finally:
         p.terminate()
         p.wait(10)
+
+
+def test_agent_auto_socket_is_private_and_reported(tmp_path):
+    """``--events auto`` binds in a fresh 0711 directory (no other user can pre-create or swap the
+    socket) and reports the path; the directory is gone when the agent exits."""
+    env = {**os.environ, "XDG_RUNTIME_DIR": str(tmp_path)}
+    p = subprocess.Popen([sys.executable, "-m", "tensorhive_fixed_amd.agent", "--stream", "2000", "--backend", "stub",
+                          "--stub-gpus", "1", "--host", "n9", "--events", "auto"], stdout=subprocess.PIPE, text=True,
+                         env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        sock = json.loads(p.stdout.readline())["events_socket"]
+        d = os.path.dirname(sock)
+        assert os.path.dirname(d) == str(tmp_path) and os.path.basename(d).startswith("tensorhive-events-")
+        assert (os.stat(d).st_mode & 0o777) == 0o711
+        assert "entry" in json.loads(p.stdout.readline())
+        c = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
+        c.sendto(b'{"event": "task_exit", "name": "tensorhive_task_4", "exit_code": 0}', sock)
+        json.loads(p.stdout.readline())
+        assert json.loads(p.stdout.readline())["event"]["name"] == "tensorhive_task_4"
+    finally:
+        p.terminate()
+        p.wait(10)
+    assert not os.path.exists(d)
+
+
+def test_squatted_socket_path_is_never_handed_to_tasks(tmp_path):
+    """An explicit path another process already holds: the agent warns and binds nothing, so it reports no
+    socket and the daemon passes no --notify path for that node (exits are found by polling)."""
+    from tensorhive_fixed_amd.core.telemetry import RemoteBackend
+
+    squat = str(tmp_path / "ev.sock")
+    with open(squat, "w") as f:
+        f.write("not a socket")
+    argv = [sys.executable, "-m", "tensorhive_fixed_amd.agent", "--stream", "300", "--backend", "stub", "--stub-gpus",
+            "1", "--host", "n9", "--events", squat]
+
+    class T:
+        def get(self, host):
+            return self
+
+        def stream_argv(self, cmd):
+            return argv
+
+    b = RemoteBackend(T(), stream_ms=300, mode="agent")
+    try:
+        t0 = time.time()
+        while b.sample("n9") is None and time.time() - t0 < 20:
+            time.sleep(0.1)
+        assert b.sample("n9") is not None
+        assert b.event_socket("n9") is None
+    finally:
+        b.close()
+    # and a well-behaved agent's reported path is what the backend hands out
+    argv[-1] = str(tmp_path / "ok.sock")
+    b = RemoteBackend(T(), stream_ms=300, mode="agent")
+    try:
+        t0 = time.time()
+        while b.event_socket("n9") is None and time.time() - t0 < 20:
+            b.sample("n9")
+            time.sleep(0.1)
+        assert b.event_socket("n9") == str(tmp_path / "ok.sock")
+    finally:
+        b.close()
