@@ -123,6 +123,7 @@ def main() -> int:
             "attention": attention_backend(),
             "grad_bucket_mb": args.bucket_mb,
             "gemm_table": bool(getattr(tr, "gemm_table", False)),  # measured hipBLASLt/rocBLAS choices (ops/tuned)
+            "gemm_table_kind": getattr(tr, "gemm_table_name", None),
         },
         "tflops_per_gpu": round(flops / n / 1e12, 1),
         "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,

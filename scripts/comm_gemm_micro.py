@@ -11,6 +11,7 @@ from __future__ import annotations
 import json
 import os
 import sys
+import time
 
 import torch
 
@@ -26,8 +27,10 @@ DGRAD = {"wqkv": (4096, 6144), "wo": (4096, 4096), "w13": (4096, 28672), "w2": (
 
 
 def timed(fn, reps=5):
+    # current-stream syncs only: a device-wide synchronize would also wait for the channel kernel on its side
+    # stream (until its time slice ends), and the GEMMs would then run on an idle chip
     fn()
-    torch.cuda.synchronize()
+    torch.cuda.current_stream().synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best = []
     for _ in range(reps):
@@ -54,8 +57,9 @@ def main():
     for k in ks:
         emu = CommEmulator(parse(f"cus={k},copy=1,slice_ms=9000,buffer_mb=64"), dev) if k else None
         if emu is not None:
-            emu.bucket_ready(1)  # resident until stop()
-            torch.cuda.synchronize()
+            emu.bucket_ready(1)  # resident until stop() (or 9 s)
+            time.sleep(0.05)  # the channel workgroups are on their CUs before the first GEMM
+
         rows = []
         if "tn" in what:
             for name, (m, n) in WGRAD.items():

@@ -71,15 +71,16 @@ def make(kind, M, N, K, res, dev, name=""):
 
 
 def timeit(fn, iters=20):
+    # current-stream syncs: a device-wide one would wait for TH_TUNE_EMU's channel kernel on its side stream
     for _ in range(3):
         fn()
-    torch.cuda.synchronize()
+    torch.cuda.current_stream().synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(iters):
         fn()
     e.record()
-    torch.cuda.synchronize()
+    e.synchronize()
     return s.elapsed_time(e) / iters
 
 
@@ -116,8 +117,8 @@ def main():
 
         _lib.load()
         emu = CommEmulator(parse(os.environ["TH_TUNE_EMU"] + ",copy=1,slice_ms=5000,buffer_mb=64"), torch.device("cuda"))
-        emu.hold(float(os.environ.get("TH_TUNE_EMU_S", "1500")))
-        torch.cuda.synchronize()
+        emu.hold(float(os.environ.get("TH_TUNE_EMU_S", "700")))
+        time.sleep(0.05)  # channel workgroups resident before the first GEMM
     try:
         _run(mode, tun)
     finally:

@@ -280,14 +280,18 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   // lane holds C[m = 16 i + r16][n = 16 j + 4 g4 .. +3] of the wave tile
   const int r16 = lane & 15, g4 = lane >> 4;
   const long crow0 = m0 + wm * 128, ccol0 = n0 + wn * 128;
+  // (with both epilogues in one kernel the compiler spills 3-4 accumulators around the bf16 path's
+  // conversion: 36-68 B of scratch per lane, after the main loop only)
   if (is_piece) {
     // tile-local slab: [split tile][split][256][256] f32, so a launch needs split tiles * splitk * 64 K floats
     float* ts = slab + ((long)(tile - full) * splitk + split) * (TM * TN) + (wm * 128) * TN + wn * 128;
+    // stored straight from the AGPRs
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        *reinterpret_cast<f32x4*>(ts + (16 * i + r16) * TN + 16 * j + 4 * g4) = acc[i][j];
+        asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(ts + (16 * i + r16) * TN + 16 * j + 4 * g4),
+                     "a"(acc[i][j]) : "memory");
     return;
   }
   char LDS_AS* ep = (char LDS_AS*)smem_raw + w * 32768;

@@ -8,6 +8,7 @@ K not a multiple of 64 x split) fall back to ``torch.mm``.
 """
 from __future__ import annotations
 
+import functools
 import os
 from contextlib import contextmanager
 
@@ -87,12 +88,24 @@ def tn_plan(m: int, n: int, k: int, cus: int | None = None) -> tuple[int, int]:
     ``TH_GEMM_TN_SPLITK`` forces the split factor (every tile split).  At 256 CUs this reproduces the round-5
     choices on every Llama-3-8B weight-gradient shape (tests/test_gemm_tn_cpu.py)."""
     cmin = compute_cus() if cus is None else int(cus)
-    tiles = (m // _TILE) * (n // _TILE)
     env = os.environ.get("TH_GEMM_TN_SPLITK")
     if env:
         s = int(env)
-        return s, (tiles if s == 1 else 0)
+        return s, ((m // _TILE) * (n // _TILE) if s == 1 else 0)
+    return _tn_plan(m, n, k, cmin)
+
+
+@functools.lru_cache(maxsize=1024)
+def _tn_plan(m: int, n: int, k: int, cmin: int) -> tuple[int, int]:
+    """Cached: the list-schedule model runs in Python and a launch must not wait for it (the step issues
+    ~130 TN launches; planning each one again cost milliseconds of host time per launch)."""
+    tiles = (m // _TILE) * (n // _TILE)
     cs = sorted({cmin, _CHIP_CUS}) if cmin < _CHIP_CUS else [cmin]
+    if tiles > 2 * cmin:
+        # measured (profiles/r06_comm/micro2): with 8-32 CUs held, the 256-CU plan of the gate|up (1792 tiles)
+        # and down (896) gradients beats every re-plan (6.0 vs 6.1 ms, 2.9 vs 3.2 ms): their split pieces cost
+        # more than the spilled round; only wo (256 tiles) and wqkv (384) gain (0.93 vs 1.25, 1.49 vs 1.63 ms)
+        cs = [_CHIP_CUS]
 
     def cost(s: int, full: int) -> float:
         return sum(plan_time(tiles, s, full, c) / (tiles / c) for c in cs) / len(cs)

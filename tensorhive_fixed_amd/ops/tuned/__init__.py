@@ -19,8 +19,18 @@ HERE = Path(__file__).resolve().parent
 TABLE = HERE / "gemm_gfx950_t32768.csv"
 
 
+def table_path(path: str | os.PathLike | None = None) -> Path:
+    """The table :func:`load_gemm_table` reads: ``path``, else ``TH_GEMM_TUNED_FILE``, else the shipped one."""
+    return Path(path or os.environ.get("TH_GEMM_TUNED_FILE", TABLE))
+
+
 def load_gemm_table(path: str | os.PathLike | None = None) -> bool:
     """Enable TunableOp in lookup-only mode with the tuned table (``TH_GEMM_TUNED=0`` disables).
+
+    Multi-rank steps use the same table.  A table tuned while an emulated RCCL channel kernel held 16 CUs
+    (replacing hipBLASLt's stream-K defaults, whose one-workgroup-per-CU grids double when CUs are held) measured
+    worse in the step on an idle chip (w13 input gradient 5.09 -> 5.89 ms) and no better under held CUs with
+    the channels' HBM traffic (10.6 ms for its MT192x256 kernel against 5.8 for stream-K): profiles/r06_comm/.
 
     On the round-5 table: -5.1 ms per step (three interleaved pairs: -3.8 / -4.5 / -7.1 ms), mostly the
     gate|up forward GEMM on a rocBLAS solution (5.11 -> 5.00 ms); the w13 input-gradient entry is pinned to
@@ -29,7 +39,7 @@ def load_gemm_table(path: str | os.PathLike | None = None) -> bool:
         return False
     import torch
 
-    p = Path(path or os.environ.get("TH_GEMM_TUNED_FILE", TABLE))
+    p = table_path(path)
     if not torch.cuda.is_available() or not p.exists():
         return False
     tun = torch.cuda.tunable

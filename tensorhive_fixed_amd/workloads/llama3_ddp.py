@@ -106,7 +106,10 @@ class Trainer:
         if dev.type == "cuda":
             from ..ops.tuned import load_gemm_table
 
+            from ..ops.tuned import table_path
+
             self.gemm_table = load_gemm_table()  # measured hipBLASLt / rocBLAS choices (TH_GEMM_TUNED)
+            self.gemm_table_name = table_path().name if self.gemm_table else None
         self.zero = default_zero(info.world) if zero is None else zero
         self.model = Llama(cfg, device=dev, dtype=torch.bfloat16, seed=seed)
         self.store = FlatParamStore(self.model.params_in_backward_order(), dev, bucket_mb=bucket_mb,

@@ -27,3 +27,4 @@ def test_loader_is_off_without_a_gpu_or_when_disabled(monkeypatch):
         assert tuned.load_gemm_table() is False
     monkeypatch.setenv("TH_GEMM_TUNED", "0")
     assert tuned.load_gemm_table() is False
+
