@@ -140,7 +140,8 @@ def authorized_keys_lists_key(username: str, key_path: str) -> tuple[bool, str]:
     sshdir, ak = home / ".ssh", home / ".ssh" / "authorized_keys"
     for p, what in ((home, "home directory"), (sshdir, "~/.ssh"), (ak, "authorized_keys")):
         try:
-            info = os.lstat(p)
+            # the home directory may be a symlink (/home -> /data/home): judged by what it points to
+            info = os.stat(p) if p == home else os.lstat(p)
         except OSError:
             return False, f"{what} is not readable by the daemon"
         if st.S_ISLNK(info.st_mode):

@@ -10,9 +10,10 @@
 // column-wise with the hardware transpose read ds_read_b64_tr_b16.
 //
 // One schedule ("hb", gemm_tn_hb_kernel below): 256 x 256 x 64 tiles on one wave per SIMD, the loop shape
-// of hipBLASLt's gfx950 MT256x256x64 kernels.  Launch modes: whole-K tiles, split-K into an f32 slab + a
-// reduce, or whole tiles data-parallel on every CU with only the remainder tiles split-K.  Output tiles
-// run in XCD bands (each XCD's 4 MB L2 re-reads a compact band's k-panels).  The round-1..4 schedules
+// of hipBLASLt's gfx950 MT256x256x64 kernels.  One grid per launch: whole-K tiles first, then split-K
+// pieces of the remaining tiles into an f32 slab of those tiles + a per-tile reduce (all whole, all split,
+// or the mix ops/gemm_tn.py:tn_plan picks for the CUs the launch may meet).  Output tiles run in XCD bands
+// (each XCD's 4 MB L2 re-reads a compact band's k-panels).  The round-1..4 schedules
 // (8-wave lockstep / ping-pong, 32-deep ring, 128 x 128 waves) were retired in round 5 after hb beat
 // them on every shape: profiles/r05_gemm/ (gemm_tn_old_modes_removed.patch restores them).
 #include "th_common.h"

@@ -102,3 +102,10 @@ def test_remote_node_uses_only_the_login(home, monkeypatch):
     monkeypatch.setattr(ssh, "get_config", lambda: cfg)
     monkeypatch.setattr(ssh, "_ssh_login_ok", lambda *a: False)
     assert not ssh.verify_login_as("n1", "alice", home.key)  # a readable authorized_keys is not enough
+
+
+def test_symlinked_home_directory_is_followed(home, tmp_path):
+    link = tmp_path / "home-link"
+    link.symlink_to(home.home)
+    home.entry.pw_dir = str(link)
+    assert ssh.authorized_keys_lists_key("alice", home.key)[0]
