@@ -9,8 +9,13 @@ SINGLE=$R/tensorhive_fixed_amd/ops/tuned/gemm_gfx950_t32768.csv
 run_step r06/$T/base 300 $B; grep -o '"value": [0-9.]*' $O/base.log
 for spec in ${SPECS:-cus=8 cus=16 cus=32 cus=64 cus=16,mode=bucket cus=32,mode=bucket}; do
   n=$(echo $spec | tr ',=' '__')
-  TH_COMM_EMU="$spec" TH_COMM_CUS=0 TH_GEMM_TUNED_FILE=$SINGLE run_step r06/$T/${n}_nofix 300 $B
+  # nofix: round-5 behaviour (stream-K grids as hipBLASLt picks them, TN planned for 256 CUs)
+  TENSILE_STREAMK_DATA_PARALLEL=0 TH_COMM_EMU="$spec" TH_COMM_CUS=0 TH_GEMM_TUNED_FILE=$SINGLE run_step r06/$T/${n}_nofix 300 $B
   echo "$n nofix $(grep -o '"value": [0-9.]*' $O/${n}_nofix.log)"
+  # default: the shipped multi-rank settings (stream-K kernels tiled data-parallel, TN planned for 256 CUs)
+  TH_COMM_EMU="$spec" TH_COMM_CUS=0 run_step r06/$T/${n}_default 300 $B
+  echo "$n default $(grep -o '"value": [0-9.]*' $O/${n}_default.log)"
+  # fix: + the TN launch planned for the CUs the channels leave (TH_COMM_CUS, automatic under the rehearsal)
   TH_COMM_EMU="$spec" run_step r06/$T/${n}_fix 300 $B
   echo "$n fix $(grep -o '"value": [0-9.]*' $O/${n}_fix.log)"
 done

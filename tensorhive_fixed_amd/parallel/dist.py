@@ -34,6 +34,12 @@ def rccl_env_defaults() -> dict[str, str]:
         "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1",  # a dead peer aborts the job instead of hanging
         "NCCL_DEBUG": "WARN",
         "TORCH_NCCL_HIGH_PRIORITY": "1",         # comm stream gets priority over compute
+        # hipBLASLt's stream-K kernels (the default for the w13 input gradient, the w2 forward and the LM-head
+        # input gradient) launch one workgroup per CU; with RCCL's channel kernels holding CUs their share waits
+        # for a second round (w13 input gradient 5.2 -> 9.7 ms with 8 CUs held).  Data-parallel tiling keeps
+        # them robust: 6.2 ms there, the same on an idle chip (645.2 vs 645.4 ms of GEMMs per step), and the
+        # step with 16 CUs held through backward +9.3 % (profiles/r06_comm/skdp/)
+        "TENSILE_STREAMK_DATA_PARALLEL": "1",
     }
 
 
@@ -43,7 +49,7 @@ def apply_env_defaults() -> None:
 
 
 COMM_ENV_PREFIXES = ("NCCL_", "RCCL_", "TORCH_NCCL_", "HSA_ENABLE_IPC", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
-                     "TH_CPU_BIND", "GPU_MAX_HW_QUEUES")
+                     "TH_CPU_BIND", "GPU_MAX_HW_QUEUES", "TENSILE_STREAMK_")
 
 
 def comm_env() -> dict[str, str]:

@@ -47,3 +47,20 @@ def test_backward_cu_budget_policy(monkeypatch):
     assert backward_cu_budget(multi) is None and backward_cu_budget(emu) is None
     monkeypatch.setenv("TH_COMM_CUS", "250")
     assert backward_cu_budget(one) == 64  # never below 64 CUs
+
+
+def test_streamk_data_parallel_preset(monkeypatch):
+    """profiles/r06_comm/skdp: hipBLASLt's stream-K kernels tiled data-parallel -- free on an idle chip, +9 % on
+    the step with 16 CUs held; preset for every run before hipBLASLt initialises, never over a user's value."""
+    from tensorhive_fixed_amd.parallel.dist import apply_env_defaults, comm_env, rccl_env_defaults
+
+    assert rccl_env_defaults()["TENSILE_STREAMK_DATA_PARALLEL"] == "1"
+    monkeypatch.delenv("TENSILE_STREAMK_DATA_PARALLEL", raising=False)
+    apply_env_defaults()
+    import os
+
+    assert os.environ["TENSILE_STREAMK_DATA_PARALLEL"] == "1"
+    assert comm_env()["TENSILE_STREAMK_DATA_PARALLEL"] == "1"  # recorded in the bench census
+    monkeypatch.setenv("TENSILE_STREAMK_DATA_PARALLEL", "0")
+    apply_env_defaults()
+    assert os.environ["TENSILE_STREAMK_DATA_PARALLEL"] == "0"
