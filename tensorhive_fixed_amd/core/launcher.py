@@ -17,11 +17,14 @@ from __future__ import annotations
 
 import json
 
+# the payload's own presets (parallel/dist.py::rccl_env_defaults, which it applies itself when unset), written
+# into the template so a user's torchrun job sees them too; kept equal by tests/test_comm_emu.py
 RCCL_ENV = {
     "HSA_ENABLE_IPC_MODE_LEGACY": "0",
     "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1",
     "NCCL_DEBUG": "WARN",
     "TORCH_NCCL_HIGH_PRIORITY": "1",
+    "TENSILE_STREAMK_DATA_PARALLEL": "1",
 }
 
 TEMPLATES = {

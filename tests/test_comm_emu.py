@@ -64,3 +64,10 @@ def test_streamk_data_parallel_preset(monkeypatch):
     monkeypatch.setenv("TENSILE_STREAMK_DATA_PARALLEL", "0")
     apply_env_defaults()
     assert os.environ["TENSILE_STREAMK_DATA_PARALLEL"] == "0"
+
+
+def test_launcher_template_carries_the_payload_presets():
+    from tensorhive_fixed_amd.core.launcher import RCCL_ENV
+    from tensorhive_fixed_amd.parallel.dist import rccl_env_defaults
+
+    assert RCCL_ENV == rccl_env_defaults()
