@@ -522,6 +522,10 @@ class FlatAdamW:
                     st.gather_bucket(bi)
                 elif self.overlap:
                     st.mark_updated(bi)
+                if st.comm_emu is not None:
+                    # the rehearsal's ZeRO-1 parameter all-gather of this bucket (bucket mode only)
+                    b = st.buckets[bi]
+                    st.comm_emu.bucket_gathered((b.end - b.start) * st.param_buf.element_size())
 
     def grad_norm(self) -> float:
         """Global gradient norm of the last step (forces a host sync; for logging only)."""

@@ -88,3 +88,21 @@ def test_training_step_with_emulation_matches_without(monkeypatch):
             r = tr.store.comm_emu.report()
             assert r["launches"] >= 3 and r["workgroups"] == 32 * r["launches"], r
     assert losses[""] == losses["cus=32,slice_ms=20,buffer_mb=64"]
+
+
+def test_bucket_mode_emulates_reduce_scatter_and_all_gather(monkeypatch):
+    """Bucket mode: one launch per bucket for its reduce-scatter (backward) and one for its all-gather (after
+    its optimizer update); persist mode launches at bucket-ready points only."""
+    from tensorhive_fixed_amd.models.llama3 import LlamaConfig
+    from tensorhive_fixed_amd.parallel.dist import DistInfo
+    from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer
+
+    info = DistInfo(0, 0, 1, torch.device("cuda", 0), None)
+    monkeypatch.setenv("TH_COMM_EMU", "cus=8,mode=bucket,buffer_mb=32")
+    tr = Trainer(LlamaConfig.tiny(), info, micro_batch=2, seq_len=256, seed=0, bucket_mb=0.25)
+    nb = len(tr.store.buckets)
+    for _ in range(2):
+        tr.step()
+    torch.cuda.synchronize()
+    r = tr.store.comm_emu.report()
+    assert r["launches"] == 2 * 2 * nb, (r, nb)
