@@ -9,6 +9,11 @@ SINGLE=$R/tensorhive_fixed_amd/ops/tuned/gemm_gfx950_t32768.csv
 run_step r06/$T/base 300 $B; grep -o '"value": [0-9.]*' $O/base.log
 for spec in ${SPECS:-cus=8 cus=16 cus=32 cus=64 cus=16,mode=bucket cus=32,mode=bucket}; do
   n=$(echo $spec | tr ',=' '__')
+  if [ "${ONLY_DEFAULT:-0}" = "1" ]; then
+    TH_COMM_EMU="$spec" TH_COMM_CUS=0 run_step r06/$T/${n}_default 300 $B
+    echo "$n default $(grep -o '"value": [0-9.]*' $O/${n}_default.log)"
+    continue
+  fi
   # nofix: round-5 behaviour (stream-K grids as hipBLASLt picks them, TN planned for 256 CUs)
   TENSILE_STREAMK_DATA_PARALLEL=0 TH_COMM_EMU="$spec" TH_COMM_CUS=0 TH_GEMM_TUNED_FILE=$SINGLE run_step r06/$T/${n}_nofix 300 $B
   echo "$n nofix $(grep -o '"value": [0-9.]*' $O/${n}_nofix.log)"
