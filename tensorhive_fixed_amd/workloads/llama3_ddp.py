@@ -70,16 +70,14 @@ def backward_cu_budget(store: FlatParamStore) -> int | None:
     ``cu_budget``), or None for the whole chip.
 
     ``TH_COMM_CUS`` names the CUs the gradient collectives hold while they run (0 = plan for all 256).
-    Unset, it is the emulated channel count when ``TH_COMM_EMU`` rehearses RCCL's footprint on one GPU,
-    and ``NCCL_MAX_NCHANNELS`` (one workgroup = one CU per channel) on a real multi-rank run, where
-    ``parallel/dist.py`` presets it.  Measured on one MI355X in profiles/r06_comm/."""
+    Unset, it is the emulated channel count when ``TH_COMM_EMU`` rehearses RCCL's footprint on one GPU, and
+    0 otherwise: on a real multi-rank step the collectives hold CUs only while they run (~4 % of the step at
+    300 GB/s), and the re-plan costs more on the idle rest than it saves (profiles/r06_comm/sweep2-5)."""
     env = os.environ.get("TH_COMM_CUS")
     if env is not None:
         reserved = int(env)
     elif store.comm_emu is not None:
         reserved = store.comm_emu.cfg.cus
-    elif store.collectives and store.world > 1:
-        reserved = int(os.environ.get("NCCL_MAX_NCHANNELS", "0") or 0)
     else:
         reserved = 0
     if reserved <= 0:

@@ -27,9 +27,9 @@ def test_no_emulator_on_cpu(monkeypatch):
 
 
 def test_backward_cu_budget_policy(monkeypatch):
-    """Rehearsal: the emulated channel count; a real multi-rank run: only an explicit TH_COMM_CUS or
-    NCCL_MAX_NCHANNELS changes the 256-CU plan (profiles/r06_comm/: the re-plan costs more on the idle chip than
-    it saves in the modelled 8-rank schedule); one rank: never."""
+    """Rehearsal: the emulated channel count; otherwise only an explicit TH_COMM_CUS changes the 256-CU plan
+    (profiles/r06_comm/: the re-plan costs more on the idle chip than it saves in the modelled 8-rank schedule),
+    a channel cap included."""
     from types import SimpleNamespace
 
     from tensorhive_fixed_amd.workloads.llama3_ddp import backward_cu_budget
@@ -42,7 +42,9 @@ def test_backward_cu_budget_policy(monkeypatch):
     assert backward_cu_budget(one) is None and backward_cu_budget(multi) is None
     assert backward_cu_budget(emu) == 224
     monkeypatch.setenv("NCCL_MAX_NCHANNELS", "16")
-    assert backward_cu_budget(multi) == 240 and backward_cu_budget(one) is None
+    assert backward_cu_budget(multi) is None and backward_cu_budget(one) is None
+    monkeypatch.setenv("TH_COMM_CUS", "16")
+    assert backward_cu_budget(multi) == 240
     monkeypatch.setenv("TH_COMM_CUS", "0")
     assert backward_cu_budget(multi) is None and backward_cu_budget(emu) is None
     monkeypatch.setenv("TH_COMM_CUS", "250")
