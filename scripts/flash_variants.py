@@ -14,10 +14,12 @@ from tensorhive_fixed_amd.ops.attention import attention_reference, flash_bwd, f
 
 def main():
     _lib.load()
-    B, S, Hq, Hkv, D = 4, 4096, 32, 8, 128
+    B, S, Hq, Hkv, D = int(os.environ.get("B", "4")), 4096, 32, 8, 128
     torch.manual_seed(0)
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
     flops = 4 * B * Hq * S * S * D / 2
+    if os.environ.get("NO_BWD"):
+        globals()["bwd_time"] = lambda *a: None
     variants = [int(v) for v in os.environ.get("VARIANTS", "11").split(",")]
     # reference on batch 0, first 1024 queries
     Sr = 1024

@@ -90,7 +90,8 @@ def flash_fwd(qkv: torch.Tensor, B: int, S: int, Hq: int, Hkv: int, Dh: int,
     v = k + Hkv * Dh * 2
     _lib.call("th_flash_attn_fwd", q, k, v, o.data_ptr(), lse.data_ptr(), B, S, Hq, Hkv, Dh,
               int(causal), row, S * row, Hq * Dh, S * Hq * Dh, 1.0 / math.sqrt(Dh),
-              0 if variant is None else 16 + (int(variant) & 15) + 32 * ((int(variant) >> 4) & 1),
+              0 if variant is None else (64 if variant == 64 else
+                                         16 + (int(variant) & 15) + 32 * ((int(variant) >> 4) & 1)),
               _lib.stream_ptr(qkv.device))
     return o, lse
 

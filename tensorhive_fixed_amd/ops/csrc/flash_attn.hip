@@ -486,6 +486,311 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------ ping-pong forward (flags bit 6)
+// Diagnostic build only (-DTH_FA_DIAG): measured 9-16 % slower than fa_fwd_kernel at the training shape in
+// every configuration tried (profiles/r06_flash/README.md).
+#ifdef TH_FA_DIAG
+// One workgroup = 8 waves = the same 128 queries of TWO query heads of one GQA group: waves 0-3 head 2p,
+// waves 4-7 head 2p + 1 of kv head hk.  Waves w and w + 4 share a SIMD and cover the same 32 query rows, so
+// their causal extents and masks are identical, and every K/V tile in LDS serves both heads (half the DMA
+// per query of fa_fwd_kernel).  The two halves run one s_barrier apart: while one half issues its MFMA
+// segment (S_i = K_i Q^T, then O^T += V_{i-1}^T P_{i-1}^T, 32 MFMAs) its SIMD partner runs its VALU segment
+// (softmax of S_i, tile DMA, the next segment's first LDS operands), then they swap, so each SIMD's matrix
+// pipe is fed by one of its two waves in every phase (MI355X_MICROARCH 'Two waves per SIMD';
+// the free-running two-workgroup pairing of fa_fwd_kernel lets both waves of a SIMD sit in softmax at once).
+//
+// LDS: a ring of PP_R units of 32 KB; unit u (slot u % PP_R) = K_u (bytes 0-16K, loaded by waves 0-3) and
+// V_{u-1} (16-32K, waves 4-7) -- exactly what MFMA segment u reads, so a unit is born and retired as one.
+// Phases (A = waves 0-3, B = 4-7): A's MFMA segment i is phase 2i and its VALU segment 2i + 1; B's are
+// 2i + 1 and 2i + 2.  Unit u is read from phase 2u - 1 (operand prefetch) to 2u + 1, so it must be
+// visible at the barrier ending phase 2u - 2: A waits for it at the end of MFMA segment u - 1, B at the end
+// of VALU segment u - 2.  Step i issues unit i + 3 (TH_PP_NMF pieces in the MFMA gaps of its S chain, the
+// rest in its VALU segment) into the slot of unit i - 1, last read at phase 2i - 1.
+constexpr int PP_R = 4, PP_SLOT = 2 * F_BN * 256;
+#ifndef TH_PP_PRIO
+#define TH_PP_PRIO 0
+#endif
+#ifndef TH_PP_SHIFT
+#define TH_PP_SHIFT 0
+#endif
+#ifndef TH_PP_NMF
+#define TH_PP_NMF 0  // of a unit's 4 DMA pieces per wave, how many go into the MFMA gaps (the rest: VALU segment)
+#endif
+#ifndef TH_PP_YPRIO
+#define TH_PP_YPRIO 0  // static s_setprio 1 for waves 4-7 (MI355X_MICROARCH 'Two waves per SIMD' item 4)
+#endif
+#ifdef TH_PP_STAMP
+// diagnostic build only: s_memtime at the segment boundaries of workgroup 0 (the heaviest q block),
+// kept in spare LDS while the kernel runs (an LDS write does not disturb the counted vmcnt waits)
+constexpr int PP_STAMP_STEPS = 72;
+__device__ unsigned long long th_pp_stamp_buf[8 * PP_STAMP_STEPS * 5];
+#define PP_STAMP(i, k)                                                                                  \
+  do {                                                                                                  \
+    if (blockIdx.x == 0 && lane == 0 && (i) < PP_STAMP_STEPS)                                           \
+      stamp_lds[(wu * PP_STAMP_STEPS + (i)) * 5 + (k)] = __builtin_amdgcn_s_memtime();                  \
+  } while (0)
+#else
+#define PP_STAMP(i, k) \
+  do {                 \
+  } while (0)
+#endif
+
+// does this wave load pieces of unit u (T key tiles -> units 0..T)?
+__device__ __forceinline__ bool pp_has(int wu, int u, int T) { return wu < 4 ? u < T : (u >= 1 && u <= T); }
+// wait until this wave's pieces of unit `need` have landed, given units up to `last` issued (`part` of
+// unit last's 4 pieces so far)
+__device__ __forceinline__ void pp_wait(int wu, int need, int last, int part, int T) {
+  if (need > T) return;
+  int n = 0;
+  for (int u = need + 1; u <= last; ++u) n += pp_has(wu, u, T) ? (u == last ? part : 4) : 0;
+  if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void pp_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(512, 1) void fa_fwd_pp_kernel(
+    const ushort* __restrict__ Q, const ushort* __restrict__ K, const ushort* __restrict__ V,
+    ushort* __restrict__ O, float* __restrict__ LSE, int B, int S, int Hq, int Hkv, long ld,
+    long bs, long ldo, long bso, float scale_log2, int causal) {
+  __shared__ __attribute__((aligned(1024))) char smem[PP_R * PP_SLOT];
+#ifdef TH_PP_STAMP
+  __shared__ unsigned long long stamp_lds[8 * PP_STAMP_STEPS * 5];
+#endif
+  const int G = Hq / Hkv, P = G >> 1;
+  const int nqb = (S + F_BM - 1) / F_BM;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = nqb * P, grp = L / per, r = L % per;
+  const int b = grp / Hkv, hk = grp % Hkv, qb = nqb - 1 - r / P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const bool half = wu >= 4;
+  const int hq = hk * G + 2 * (r % P) + (half ? 1 : 0);
+  const int q0 = qb * F_BM + (wu & 3) * 32;  // wave-uniform (scalar branches on it)
+  const int q = q0 + c32;
+  const ushort* Qb = Q + b * bs + (long)hq * HD;
+  const ushort* Kb = K + b * bs + (long)hk * HD;
+  const ushort* Vb = V + b * bs + (long)hk * HD;
+
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    ushort8 u = q < S ? *reinterpret_cast<const ushort8*>(Qb + (long)q * ld + 16 * s + 8 * h) : ushort8(0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale_log2);
+    qf[s] = as_bf(u);
+  }
+  const int kv_end = causal ? min(S, qb * F_BM + F_BM) : S;
+  const int T = (kv_end + F_BN - 1) / F_BN;
+  unsigned rc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) rc[u] = img_rc((w & 3) * 4096 + u * 1024 + lane * 16);
+  const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem + (half ? F_BN * 256 : 0) + (wu & 3) * 4096;
+  const ushort* src = half ? Vb : Kb;
+  // piece p (of 4) of this wave's share of unit u: K rows of tile u (A) or V rows of tile u - 1 (B)
+  auto issue_piece = [&](int u, int p) {
+    if (u > T || !pp_has(wu, u, T)) return;
+    const int tile = half ? u - 1 : u;
+    const int row = min(tile * F_BN + (int)(rc[p] & 255), S - 1);
+    glds16(src, (unsigned)(row * ld + (rc[p] >> 8) * 8) * 2u, lds0 + (u % PP_R) * PP_SLOT + p * 1024);
+  };
+  auto issue = [&](int u) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue_piece(u, p);
+  };
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q loads retired by a wait the compiler sees (vmcnt(0))
+  issue(0);
+  issue(1);
+  issue(2);
+  pp_wait(wu, 0, min(2, T), 4, T);
+  pp_barrier();
+
+  auto kimg = [&](int u) { return smem + (u % PP_R) * PP_SLOT; };
+  // this wave's key tiles 0 .. Tw - 1 (wave-uniform; the tiles above its diagonal are skipped)
+  const int Tw = causal ? min(T, (q0 + 31) / F_BN + 1) : T;
+  f32x16 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = f32x16(0.f);
+  float m_i = -INFINITY, l_i = 0.f;
+  float m_base = 0.f;  // TH_PP_SHIFT: the S chains start from s_init = -m_base (C = 0 otherwise)
+  f32x16 s_init = f32x16(0.f);  // the MFMA reads C from here: no copies
+  f32x16 sacc[2];
+  bf16x8 pf[4], ka[3][2];
+  // first two steps' operands of MFMA segment i's S chain (K_i rows), read in the VALU segment before it;
+  // V^T's first k-step is read during the chain's last steps, so 16 operand registers live across the
+  // barrier.  Unconditional: a segment without S never reads them.
+  auto prefetch = [&](int i) {
+    const char* ks = kimg(i);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      ka[t][0] = lds_row(ks, c32, 2 * t + h);
+      ka[t][1] = lds_row(ks, 32 + c32, 2 * t + h);
+    }
+  };
+  // MFMA segment i: S_i (DO_S), then PV_{i-1} (DO_PV).  Called with constant flags only, so each loop
+  // below has one straight-line body (branches inside a body cost phi copies of the operand registers).
+  auto mfma_seg = [&](int i, bool DO_S, bool DO_PV) __attribute__((always_inline)) {
+    const char* ks = kimg(i);
+    const char* vs = ks + F_BN * 256;
+    bf16x8 vt[4];
+    if (DO_S) {  // K-row operands two steps ahead of their MFMAs (one step leaves the LDS latency exposed)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s + 2 < 8) {
+          ka[(s + 2) % 3][0] = lds_row(ks, c32, 2 * s + 4 + h);
+          ka[(s + 2) % 3][1] = lds_row(ks, 32 + c32, 2 * s + 4 + h);
+        } else if (s == 6 && DO_PV) {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) vt[d] = lds_tr(vs, 0, 32 * d, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        sacc[0] = mfma(ka[s % 3][0], qf[s], s == 0 ? s_init : sacc[0]);
+        if ((s & 1) && (s >> 1) < TH_PP_NMF) issue_piece(i + 3, s >> 1);  // DMA pieces in the MFMA gaps
+        sacc[1] = mfma(ka[s % 3][1], qf[s], s == 0 ? s_init : sacc[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < TH_PP_NMF; ++p) issue_piece(i + 3, p);
+      if (DO_PV) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) vt[d] = lds_tr(vs, 0, 32 * d, lane);
+      }
+    }
+    if (DO_PV) {
+#pragma unroll
+      for (int ks4 = 0; ks4 < 4; ++ks4) {
+        bf16x8 nx[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) nx[d] = ks4 < 3 ? lds_tr(vs, 16 * ks4 + 16, 32 * d, lane) : vt[d];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = mfma(vt[d], pf[ks4], o[d]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) vt[d] = nx[d];
+      }
+    }
+  };
+  // softmax of S_i -> P_i (bf16 operands pf), running max / sum, O rescale when the max moved past 2^8
+  auto softmax = [&](int i) __attribute__((always_inline)) {
+    if (TH_PP_PRIO) __builtin_amdgcn_s_setprio(1);  // the VALU segment is the phase's critical path
+    const int kbase = i * F_BN;
+    const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);  // wave-uniform
+    if (need_mask) {
+      const int kmax = (causal ? min(q, S - 1) : S - 1) - kbase - 4 * h;  // last visible key, tile-relative
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr)
+          sacc[kb][rr] = (32 * kb + (rr & 3) + 8 * (rr >> 2) <= kmax) ? sacc[kb][rr] : -INFINITY;
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) mt = fmaxf(mt, sacc[kb][rr]);
+    mt = half_swap_max(mt);
+    if (!__all(mt + m_base - m_i <= F_DEFER_THR)) {  // DEFER of fa_fwd_kernel
+      const float m_new = fmaxf(m_i, mt + m_base);
+      const float mu = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = fast_exp2(m_i - mu);
+      l_i *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d] *= alpha;
+      m_i = m_new;
+      if (TH_PP_SHIFT) {  // rebase this tile's scores and the next chains' start
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sacc[kb] -= mu - m_base;
+        m_base = mu;
+        s_init = f32x16(-mu);
+      }
+    }
+    const float m_use = TH_PP_SHIFT ? 0.f : (m_i == -INFINITY ? 0.f : m_i);
+    float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const float p = fast_exp2(TH_PP_SHIFT ? sacc[kb][rr] : sacc[kb][rr] - m_use);
+        sacc[kb][rr] = p;
+        rs4[rr & 3] += p;
+      }
+    pf[0] = pack8(sacc[0], 0);
+    pf[1] = pack8(sacc[0], 8);
+    pf[2] = pack8(sacc[1], 0);
+    pf[3] = pack8(sacc[1], 8);
+    const float rs = (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
+    l_i += half_swap_sum(rs);
+    if (TH_PP_PRIO) {
+      if (TH_PP_YPRIO && half) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  // the two barriers of step i around the VALU segment (A waits for unit i + 1 before the first, B for
+  // unit i + 2 before the second)
+  auto sync_mid = [&](int i) {
+    if (!half) pp_wait(wu, i + 1, min(i + 3, T), i + 3 <= T ? TH_PP_NMF : 4, T);
+    pp_barrier();
+  };
+  auto sync_end = [&](int i) {
+#pragma unroll
+    for (int p = TH_PP_NMF; p < 4; ++p) issue_piece(i + 3, p);
+    if (i < T) prefetch(i + 1);
+    if (half) pp_wait(wu, i + 2, min(i + 3, T), 4, T);
+    pp_barrier();
+  };
+  prefetch(0);
+  if (TH_PP_YPRIO && half) __builtin_amdgcn_s_setprio(1);
+  if (half) pp_barrier();  // B sits out A's first MFMA segment
+
+  PP_STAMP(0, 0);
+  mfma_seg(0, true, false);
+  PP_STAMP(0, 1);
+  sync_mid(0);
+  PP_STAMP(0, 2);
+  softmax(0);
+  PP_STAMP(0, 3);
+  sync_end(0);
+  PP_STAMP(0, 4);
+  for (int i = 1; i < Tw; ++i) {
+    PP_STAMP(i, 0);
+    mfma_seg(i, true, true);
+    PP_STAMP(i, 1);
+    sync_mid(i);
+    PP_STAMP(i, 2);
+    softmax(i);
+    PP_STAMP(i, 3);
+    sync_end(i);
+    PP_STAMP(i, 4);
+  }
+  mfma_seg(Tw, false, true);  // PV of the wave's last tile
+  sync_mid(Tw);
+  sync_end(Tw);
+  for (int i = Tw + 1; i <= T; ++i) {  // tiles above this wave's diagonal: barriers and DMA only
+#pragma unroll
+    for (int p = 0; p < TH_PP_NMF; ++p) issue_piece(i + 3, p);
+    sync_mid(i);
+    sync_end(i);
+  }
+  if (!half) pp_barrier();  // match B's extra barrier
+#ifdef TH_PP_STAMP
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    for (int t = tid; t < 8 * PP_STAMP_STEPS * 5; t += 512) th_pp_stamp_buf[t] = stamp_lds[t];
+  }
+#endif
+
+  if (q < S) {
+    const float inv_l = l_i > 0.f ? 1.f / l_i : 0.f;
+    store_row_t21(O + b * bso + (long)q * ldo + (long)hq * HD, o, inv_l, h);
+    if (h == 0) LSE[((long)b * Hq + hq) * S + q] = (m_i + log2f(l_i)) * LN2;
+  }
+}
+#endif  // TH_FA_DIAG (ping-pong forward)
+
 // ------------------------------------------------------------------------------- dQ kernel
 // dQ: wave priority around the MFMA chains (round 1 measured it neutral on the older dQ body)
 #ifndef TH_DQ_PRIO_ON
@@ -1601,6 +1906,18 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
   // flags: 0 = default variant; 16 + v = explicit v (bit0 PRESCALE, bit1 DEFER, bit2 DBUF,
   // bit3 KVMAJOR block order)
   // flags bit5 (with 16 + v): SPREAD on the DMA variants (default: TH_FA_FWD_SPREAD)
+  if (flags & 64) {  // ping-pong kernel (diagnostic build): two query heads per workgroup, 32-bit DMA offsets
+#ifdef TH_FA_DIAG
+    if ((Hq / Hkv) % 2 != 0 || (long)S * ld * 2 >= (1L << 31)) return -3;
+    const long npp = (long)((S + F_BM - 1) / F_BM) * (Hq / 2) * B;
+    fa_fwd_pp_kernel<<<(unsigned)npp, 512, 0, s>>>((const ushort*)q, (const ushort*)k, (const ushort*)v,
+                                                    (ushort*)o, lse, B, S, Hq, Hkv, ld, bs, ldo, bso,
+                                                    scale * LOG2E, causal);
+    TH_CHECK_LAUNCH();
+#else
+    return -3;
+#endif
+  }
   int var = flags >= 16 ? (flags & 15) : TH_FA_FWD_DEFAULT;
   bool spread = flags >= 16 ? ((flags >> 5) & 1) : TH_FA_FWD_SPREAD;
   if ((long)S * ld * 2 >= (1L << 31)) var &= ~4;  // DMA staging uses 32-bit row offsets
@@ -1641,6 +1958,12 @@ extern "C" int th_flash_attn_fwd(const void* q, const void* k, const void* v, vo
 #undef TH_FWD
   TH_CHECK_LAUNCH();
 }
+
+#ifdef TH_PP_STAMP
+extern "C" int th_pp_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(th_pp_stamp_buf), sizeof(th_pp_stamp_buf));
+}
+#endif
 
 // rcos / rsin (the [S][64] rotary tables, or null): the rotary backward of dQ and dK is applied in the
 // dQ and dK|dV kernels' epilogues (default dK|dV kernel only: other flags return -3 with tables given)

@@ -178,3 +178,50 @@ def test_retired_backward_flags_are_rejected(flags):
     o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D)
     with pytest.raises(RuntimeError, match="bad shape"):
         flash_bwd(torch.randn_like(o), qkv, o, lse, B, S, Hq, Hkv, D, flags=flags)
+
+
+# The 8-wave ping-pong forward (flags bit 6) lost to the default kernel (profiles/r06_flash/) and lives in the
+# diagnostic library only: its numerics run when TH_KERNEL_LIB points at one (scripts/build_variant_lib.sh
+# fa_diag -DTH_FA_DIAG=1), and the production library must refuse the flag.
+_DIAG_LIB = "diag" in __import__("os").environ.get("TH_KERNEL_LIB", "")
+
+
+@pytest.mark.skipif(not _DIAG_LIB, reason="ping-pong forward: diagnostic library only")
+@pytest.mark.parametrize("causal", [True, False], ids=["causal", "full"])
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(1, 128, 4, 1), (2, 200, 8, 2), (1, 1024, 32, 8), (3, 192, 4, 2),
+                                        (2, 320, 6, 3), (1, 4096, 32, 8), (1, 8192, 8, 2)])
+def test_pingpong_forward_matches_default_and_fp32(B, S, Hq, Hkv, causal):
+    """The 8-wave ping-pong forward (flags bit 6): same output as the default kernel, fp32 reference on one
+    GQA group (chunked for the long shapes), S % 64 != 0 and non-causal included."""
+    from tensorhive_fixed_amd.ops.attention import _split, flash_fwd
+    torch.manual_seed(5)
+    D = 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+    o, lse = flash_fwd(qkv, B, S, Hq, Hkv, D, causal=causal, variant=64)
+    o_d, lse_d = flash_fwd(qkv, B, S, Hq, Hkv, D, causal=causal)
+    assert (o.float() - o_d.float()).abs().max().item() < 1e-2
+    assert (lse - lse_d).abs().max().item() < 1e-4
+    rep = Hq // Hkv
+    kv = Hkv - 1  # last group: the highest query heads of the last workgroup pair
+    q, k, v = _split(qkv.float(), B, S, Hq, Hkv, D)
+    qg = q[:, :, kv * rep:(kv + 1) * rep].transpose(1, 2)
+    kg, vg = k[:, :, kv:kv + 1].transpose(1, 2), v[:, :, kv:kv + 1].transpose(1, 2)
+    s = (qg @ kg.transpose(-1, -2)) / math.sqrt(D)
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device="cuda").triu(1), float("-inf"))
+    og = (torch.softmax(s, -1) @ vg).transpose(1, 2).reshape(B * S, rep * D)
+    sl = slice(kv * rep * D, (kv + 1) * rep * D)
+    rel = ((o[:, sl].float() - og).norm() / og.norm()).item()
+    assert rel < 1e-2, f"fwd rel err {rel}"
+    lse_ref = torch.logsumexp(s, -1)  # [B, rep, S]
+    assert (lse[:, kv * rep:(kv + 1) * rep] - lse_ref).abs().max().item() < 1e-2
+
+
+def test_pingpong_forward_refused_by_production_or_odd_groups():
+    """Production: flag 64 is refused outright; diagnostic library: refused for an odd GQA group."""
+    from tensorhive_fixed_amd.ops.attention import flash_fwd
+    B, S, D = 1, 128, 128
+    for Hq, Hkv in ((3, 1),) + (() if _DIAG_LIB else ((4, 2),)):
+        qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16)
+        with pytest.raises(RuntimeError, match="bad shape"):
+            flash_fwd(qkv, B, S, Hq, Hkv, D, variant=64)
