@@ -130,6 +130,8 @@ class _Bucket:
     handle: object = None  # gradient collective of this micro-batch
     gather: object = None  # parameter all-gather in flight (sharded mode)
     updated: object = None  # event: this bucket's optimizer update done (overlapped optimizer)
+    emu_done: object = None  # rehearsal (TH_COMM_EMU deps=1): the modelled reduce-scatter's end
+    emu_gathered: object = None  # rehearsal (TH_COMM_EMU deps=1): the modelled all-gather's end
 
     def shard(self, rank: int, world: int) -> tuple[int, int]:
         n = (self.end - self.start) // world
@@ -259,7 +261,7 @@ class FlatParamStore:
             if self.collectives:
                 b.handle = self._launch_grad_collective(b)
             if self.comm_emu is not None:
-                self.comm_emu.bucket_ready((b.end - b.start) * self.grad_buf.element_size())
+                b.emu_done = self.comm_emu.bucket_ready((b.end - b.start) * self.grad_buf.element_size())
             if self.ready_hook is not None:
                 self.ready_hook(b)
 
@@ -316,7 +318,17 @@ class FlatParamStore:
             if b is not None:
                 self._wait_bucket(b)
 
+    def wait_emu_reduced(self) -> None:
+        """Rehearsal with ``deps=1``: the current stream waits for every bucket's modelled reduce-scatter."""
+        for b in self.buckets:
+            if b.emu_done is not None:
+                torch.cuda.current_stream(self.device).wait_event(b.emu_done)
+                b.emu_done = None
+
     def _wait_bucket(self, b: _Bucket) -> None:
+        if b.emu_gathered is not None:
+            torch.cuda.current_stream(self.device).wait_event(b.emu_gathered)
+            b.emu_gathered = None
         if b.gather is not None:
             with self.timer.span("allgather"):
                 b.gather.wait()
@@ -484,6 +496,7 @@ class FlatAdamW:
         st = self.store
         scale = 1.0 / st.world
         groups = self._launch_groups()
+        st.wait_emu_reduced()  # rehearsal (deps=1): the norm and the update need every reduce-scatter
         early = self.early_sumsq and len(self._early_done) == len(st.buckets)
         self._early_done.clear()
         if self.clip > 0 and early:
@@ -525,7 +538,7 @@ class FlatAdamW:
                 if st.comm_emu is not None:
                     # the rehearsal's ZeRO-1 parameter all-gather of this bucket (bucket mode only)
                     b = st.buckets[bi]
-                    st.comm_emu.bucket_gathered((b.end - b.start) * st.param_buf.element_size())
+                    b.emu_gathered = st.comm_emu.bucket_gathered((b.end - b.start) * st.param_buf.element_size())
 
     def grad_norm(self) -> float:
         """Global gradient norm of the last step (forces a host sync; for logging only)."""

@@ -106,3 +106,24 @@ def test_bucket_mode_emulates_reduce_scatter_and_all_gather(monkeypatch):
     torch.cuda.synchronize()
     r = tr.store.comm_emu.report()
     assert r["launches"] == 2 * 2 * nb, (r, nb)
+
+
+def test_bucket_mode_dependencies_keep_numerics_and_order(monkeypatch):
+    """deps=1: the optimizer waits for every modelled reduce-scatter and each forward layer for its modelled
+    all-gather (events on the emulator's stream); the trajectory equals the run without emulation."""
+    from tensorhive_fixed_amd.models.llama3 import LlamaConfig
+    from tensorhive_fixed_amd.parallel.dist import DistInfo
+    from tensorhive_fixed_amd.workloads.llama3_ddp import Trainer
+
+    info = DistInfo(0, 0, 1, torch.device("cuda", 0), None)
+    losses = {}
+    for spec in ("", "cus=16,mode=bucket,busbw=5,buffer_mb=32,deps=1"):  # 5 GB/s: collectives far longer than compute
+        monkeypatch.setenv("TH_COMM_EMU", spec)
+        tr = Trainer(LlamaConfig.tiny(), info, micro_batch=2, seq_len=256, seed=0, bucket_mb=0.25)
+        losses[spec] = [float(tr.step()) for _ in range(3)]
+        torch.cuda.synchronize()
+        if spec:
+            assert all(b.emu_done is None for b in tr.store.buckets)  # every reduce-scatter was waited on
+            r = tr.store.comm_emu.report()
+            assert r["launches"] == 2 * 3 * len(tr.store.buckets), r
+    assert losses[""] == losses["cus=16,mode=bucket,busbw=5,buffer_mb=32,deps=1"]

@@ -10,7 +10,9 @@ def test_parse_spec():
     assert parse(None) is None and parse("") is None and parse("cus=0") is None
     c = parse("cus=32, mode=bucket,world=8,busbw=250,copy=0,slice_ms=20,buffer_mb=64")
     assert (c.cus, c.mode, c.world, c.busbw, c.copy, c.slice_ms, c.buffer_mb) == (32, "bucket", 8, 250.0, 0.0, 20.0, 64.0)
-    for bad in ("cus=300", "mode=ring", "cus=8,world=1", "cus=8,busbw=0", "nope=1", "cus="):
+    assert parse("cus=8,mode=bucket,deps=1").deps == 1 and parse("cus=8").deps == 0
+    for bad in ("cus=300", "mode=ring", "cus=8,world=1", "cus=8,busbw=0", "nope=1", "cus=", "cus=8,deps=1",
+                "cus=8,mode=bucket,deps=2"):
         with pytest.raises(ValueError):
             parse(bad)
 
