@@ -250,6 +250,11 @@ __device__ __forceinline__ void dma_kv_piece(const ushort* Kb, const ushort* Vb,
 #ifndef TH_FA_FWD_DEFAULT
 #define TH_FA_FWD_DEFAULT 15  // PRESCALE + DEFER + DMA-staged DBUF + KVMAJOR: 937 vs 829 TFLOP/s for 11 (B4 S4096, profiles/r01_flash_v3)
 #endif
+#ifndef TH_FA_FWD_AHEAD
+// K-row operand look-ahead of the forward S chain in k-steps (1 or 2).  2: fwd 1.047 / 1.055 vs 1.057 / 1.066 ms
+// (B 8 S 4096, alternating processes, profiles/r06_flash/ahead/), 200 instead of 220 VGPRs
+#define TH_FA_FWD_AHEAD 2
+#endif
 constexpr int F_BM = 128, F_BN = 64;
 constexpr float F_DEFER_THR = 8.f;  // log2 units: P may reach 2^8 before O/l are rescaled
 
@@ -355,6 +360,30 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     if (SPREAD && causal && kbase > q0 + 31) dma_kv_tile(Kb, Vb, ld, S, jd, lds0, wu, rc);  // skipped: still DMA
     if (!(causal && kbase > q0 + 31)) {  // wave-uniform: tile entirely above the diagonal is skipped
       f32x16 sacc[2] = {s_init, s_init};
+#if TH_FA_FWD_AHEAD == 2
+      {  // K-row operands read two k-steps ahead of the MFMAs that use them (ring of 3)
+        FA_PRIO(1);
+        bf16x8 ka[3][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          ka[t][0] = lds_row(ks, c32, 2 * t + h);
+          ka[t][1] = lds_row(ks, 32 + c32, 2 * t + h);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          if (s + 2 < 8) {
+            ka[(s + 2) % 3][0] = lds_row(ks, c32, 2 * s + 4 + h);
+            ka[(s + 2) % 3][1] = lds_row(ks, 32 + c32, 2 * s + 4 + h);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          sacc[0] = mfma(ka[s % 3][0], qf[s], sacc[0]);
+          if (SPREAD) dma_kv_piece(Kb, Vb, ld, S, jd, lds0, wu, rc, s);
+          sacc[1] = mfma(ka[s % 3][1], qf[s], sacc[1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        FA_PRIO(0);
+      }
+#else
       {  // K-row operands are read one k-step ahead of the MFMAs that use them
         FA_PRIO(1);
         bf16x8 a0 = lds_row(ks, c32, h), a1 = lds_row(ks, 32 + c32, h);
@@ -375,6 +404,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         }
         FA_PRIO(0);
       }
+#endif
       const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);  // wave-uniform
       if (!PRESCALE) {
 #pragma unroll
@@ -803,6 +833,9 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_pp_kernel(
 #ifndef TH_DQ_AHEAD
 #define TH_DQ_AHEAD 1  // 0: reads issued right before their MFMA (compiler order)
 #endif
+#ifndef TH_DQ_TR_AHEAD
+#define TH_DQ_TR_AHEAD 1  // K^T operand look-ahead of the dQ chain in d-steps (1 or 2)
+#endif
 // SPREAD (with DMA): tile j+1's 8 LDS-DMA pieces issued one per MFMA pair of the first S|dP chain
 // (no VALU there) instead of 8 in a row after the barrier -- the kf lesson: a piece costs the issuing
 // wave 60-185 cycles (profiles/r04_flash/)
@@ -965,6 +998,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
       }
       const bf16x8 s0 = pack8(sacc, 0), s1 = pack8(sacc, 8);
 #if TH_DQ_AHEAD
+#if TH_DQ_TR_AHEAD == 2
+      {  // K^T operands two d-steps ahead (ring of 3)
+        bf16x8 kt[3][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          kt[t][0] = lds_tr(ks, 32 * kb, 32 * t, lane);
+          kt[t][1] = lds_tr(ks, 32 * kb + 16, 32 * t, lane);
+        }
+        TH_DQ_PRIO(1);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (d + 2 < 4) {
+            kt[(d + 2) % 3][0] = lds_tr(ks, 32 * kb, 32 * d + 64, lane);
+            kt[(d + 2) % 3][1] = lds_tr(ks, 32 * kb + 16, 32 * d + 64, lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          dq[d] = mfma(kt[d % 3][0], s0, dq[d]);
+          dq[d] = mfma(kt[d % 3][1], s1, dq[d]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        TH_DQ_PRIO(0);
+      }
+#else
       {  // K^T operands one d-step ahead
         bf16x8 t0 = lds_tr(ks, 32 * kb, 0, lane), t1 = lds_tr(ks, 32 * kb + 16, 0, lane);
         TH_DQ_PRIO(1);
@@ -984,6 +1040,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         }
         TH_DQ_PRIO(0);
       }
+#endif
 #else
 #pragma unroll
       for (int d = 0; d < 4; ++d) {

@@ -183,7 +183,7 @@ def test_retired_backward_flags_are_rejected(flags):
 # The 8-wave ping-pong forward (flags bit 6) lost to the default kernel (profiles/r06_flash/) and lives in the
 # diagnostic library only: its numerics run when TH_KERNEL_LIB points at one (scripts/build_variant_lib.sh
 # fa_diag -DTH_FA_DIAG=1), and the production library must refuse the flag.
-_DIAG_LIB = "diag" in __import__("os").environ.get("TH_KERNEL_LIB", "")
+_DIAG_LIB = __import__("os").environ.get("TH_KERNEL_LIB", "").endswith("fa_diag.so")
 
 
 @pytest.mark.skipif(not _DIAG_LIB, reason="ping-pong forward: diagnostic library only")
