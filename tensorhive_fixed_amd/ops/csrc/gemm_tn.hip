@@ -26,6 +26,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef TH_TN_GM
 #define TH_TN_GM 8  // output-tile rows per XCD band
 #endif
+#ifndef TH_TN_M0SPLIT
+// main-loop LDS-DMA pieces: M0 written before the gap's MFMA, load after it (307 -> 282 loop instructions;
+// wqkv / wo / w2 / w13 1.185 / 0.740 / 2.656 / 5.471 -> 1.168 / 0.732 / 2.614 / 5.417 ms, alternating processes
+// on one box: profiles/r06_gemm/tn_m0split/)
+#define TH_TN_M0SPLIT 1
+#endif
 
 constexpr int TM = 256, TN = 256;
 constexpr int ROWB = TN * 2;  // bytes per LDS k-row (TM == TN)
@@ -164,6 +170,17 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   auto piece = [&](int op, int i, int kt, int st) {
     piece_at(op, i, (op == 0 ? ga : gb) + (long)kt * 64 * (op == 0 ? lda : ldb), st);
   };
+  // TH_TN_M0SPLIT: a main-loop piece in two halves -- M0 (this wave's LDS slot of the piece) written by one
+  // s_add straight into m0 BEFORE the MFMA of that gap, the buffer_load after it, so the MFMA is the
+  // wait state the M0 write needs (no s_mov / s_nop per piece: 32 fewer scalar issues per k-tile)
+  const unsigned lds_w = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)w * 1024u);
+  auto piece_load = [&](int op, int i, const ushort* base) {
+    const long ld = op == 0 ? lda : ldb;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    const unsigned soff = (unsigned)(2L * 2 * (4 * i + w) * ld);
+    const unsigned voff = op == 0 ? va[i & 3] : vb[i & 3];
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(voff), "s"(r), "s"(soff) : "memory");
+  };
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -216,9 +233,20 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const int st = t & 1;
     const char LDS_AS* s_cur = smem + st * HSTAGE;
     const char LDS_AS* s_nxt = smem + (st ^ 1) * HSTAGE;
+    const unsigned lds_stage = lds_w + (unsigned)st * HSTAGE;
     static_for_tn<0, 128>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
       constexpr int mm = m & 63, i = mm >> 3, j = mm & 7;
+      // DMA pieces spread over the whole k-tile: A's 8 every 4th MFMA from 22 (after the barrier that
+      // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
+      // (2 % faster than A every 2nd from 22 and B every 4th from 46: profiles/r05_gemm/tn_pv_sweep*.jsonl)
+      constexpr int a0 = 22, as = 4, b0 = 52, bs = 5;
+      constexpr bool pa = m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0;
+      constexpr bool pb = m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0;
+      constexpr int pi = pa ? (m - a0) / as : (pb ? (m - b0) / bs : 0);
+      constexpr int poff = (pb ? HIMG : 0) + 4096 * pi;  // piece 4 pi + w of operand A / B in the stage
+      if constexpr (TH_TN_M0SPLIT && (pa || pb))
+        asm volatile("s_add_i32 m0, %0, %1" :: "s"(lds_stage), "n"(poff) : "m0");
       if constexpr (m < 64)
         mf(acc[i][j], xb[j], xa[i]);
       else
@@ -230,11 +258,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       }
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_t = tn_stamp();
       if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      // DMA pieces spread over the whole k-tile: A's 8 every 4th MFMA from 22 (after the barrier that
-      // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
-      // (2 % faster than A every 2nd from 22 and B every 4th from 46: profiles/r05_gemm/tn_pv_sweep*.jsonl)
-      constexpr int a0 = 22, as = 4, b0 = 52, bs = 5;
-      if constexpr (m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0) piece_at(0, (m - a0) / as, pa2, st);
+      if constexpr (pa) {
+        if constexpr (TH_TN_M0SPLIT) piece_load(0, pi, pa2);
+        else piece_at(0, pi, pa2, st);
+      }
       // Y.b: 16 halves at MFMAs 23-38
       if constexpr (m >= 23 && m <= 38) {
         constexpr int h = m - 23;
@@ -242,7 +269,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
         else yb[h >> 1] = join(lo_y, rd_half(s_cur, 8 + (h >> 1), 1, 1));
       }
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if constexpr (m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0) piece_at(1, (m - b0) / bs, pb2, st);
+      if constexpr (pb) {
+        if constexpr (TH_TN_M0SPLIT) piece_load(1, pi, pb2);
+        else piece_at(1, pi, pb2, st);
+      }
       if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_w[m == 20 ? 0 : m == 44 ? 1 : 2] += tn_stamp() - d_t;
       // X of tile t+1: 32 halves at MFMAs 90-121, A0 B0-B7 A1-A7 (the next iteration starts with row 0)
