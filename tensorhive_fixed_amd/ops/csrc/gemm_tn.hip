@@ -156,6 +156,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   const unsigned lds0 = (unsigned)(uintptr_t)(char LDS_AS*)smem_raw;
   const ushort* ga = A + kbeg * lda + m0;
   const ushort* gb = B + kbeg * ldb + n0;
+  // LDS image of operand op (0 A, 1 B) in stage st: A0 | A1 | B0 | B1, 32 KB each, so the stage and operand
+  // parts of every read address are compile-time immediates below 64 KB in the two-stage unrolled loop
+  auto img = [](int op, int st) { return op * 2 * HIMG + st * HIMG; };
   // piece i of operand op of the k-tile whose first k-row is at `base`, into stage st
   auto piece_at = [&](int op, int i, const ushort* base, int st) {
     const long ld = op == 0 ? lda : ldb;
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
     const int u = 4 * i + w;
     const unsigned soff = (unsigned)(2L * 2 * u * ld);
     const unsigned voff = op == 0 ? va[i & 3] : vb[i & 3];
-    const unsigned lb = __builtin_amdgcn_readfirstlane(lds0 + st * HSTAGE + op * HIMG + u * 1024);
+    const unsigned lb = __builtin_amdgcn_readfirstlane(lds0 + img(op, st) + u * 1024);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :: "s"(lb), "v"(voff), "s"(r), "s"(soff) : "memory", "m0");
   };
@@ -206,16 +209,16 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   bf16x8 xa[8], xb[8], ya[8], yb[8];
 #pragma unroll
   for (int f = 0; f < 8; ++f) {
-    xa[f] = tr_pair(smem + a_off[f], smem + a_off[f] + 4 * ROWB);
-    xb[f] = tr_pair(smem + HIMG + b_off[f], smem + HIMG + b_off[f] + 4 * ROWB);
+    xa[f] = tr_pair(smem + img(0, 0) + a_off[f], smem + img(0, 0) + a_off[f] + 4 * ROWB);
+    xb[f] = tr_pair(smem + img(1, 0) + b_off[f], smem + img(1, 0) + b_off[f] + 4 * ROWB);
   }
   auto mf = [&](f32x4& c, const bf16x8& b, const bf16x8& a) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
   };
-  // one transposed b64 half of fragment f (0-7 A, 8-15 B) of k-step ks, stage base sb
-  auto rd_half = [&](const char LDS_AS* sb, int f, int ks, int half) -> i16x4 {
-    const int off = (f < 8 ? a_off[f] : HIMG + b_off[f - 8]) + ks * 32 * ROWB + half * 4 * ROWB;
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(sb + off));
+  // one transposed b64 half of fragment f (0-7 A, 8-15 B) of k-step ks in stage st (a constant in the loop)
+  auto rd_half = [&](int st, int f, int ks, int half) -> i16x4 {
+    const int off = (f < 8 ? a_off[f] : b_off[f - 8]) + img(f < 8 ? 0 : 1, st) + ks * 32 * ROWB + half * 4 * ROWB;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4*)(smem + off));
   };
   auto join = [](i16x4 lo, i16x4 hi2) {
     typedef short i16x8 __attribute__((ext_vector_type(8)));
@@ -229,11 +232,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   // tile is re-staged (nobody reads it)
   const ushort* pa2 = ga + (long)min(2, nt - 1) * 64 * lda;
   const ushort* pb2 = gb + (long)min(2, nt - 1) * 64 * ldb;
-  for (int t = 0; t < nt; ++t) {
-    const int st = t & 1;
-    const char LDS_AS* s_cur = smem + st * HSTAGE;
-    const char LDS_AS* s_nxt = smem + (st ^ 1) * HSTAGE;
-    const unsigned lds_stage = lds_w + (unsigned)st * HSTAGE;
+  // k-tile t in stage ST = t & 1, unrolled per stage (two k-tiles per trip, plus an even tail tile)
+  auto ktile = [&](auto stc) {
+    constexpr int ST = decltype(stc)::value;
     static_for_tn<0, 128>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
       constexpr int mm = m & 63, i = mm >> 3, j = mm & 7;
@@ -244,34 +245,34 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       constexpr bool pa = m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0;
       constexpr bool pb = m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0;
       constexpr int pi = pa ? (m - a0) / as : (pb ? (m - b0) / bs : 0);
-      constexpr int poff = (pb ? HIMG : 0) + 4096 * pi;  // piece 4 pi + w of operand A / B in the stage
+      constexpr int poff = (pb ? 2 * HIMG : 0) + ST * HIMG + 4096 * pi;  // piece 4 pi + w of A / B in stage ST
       if constexpr (TH_TN_M0SPLIT && (pa || pb))
-        asm volatile("s_add_i32 m0, %0, %1" :: "s"(lds_stage), "n"(poff) : "m0");
+        asm volatile("s_add_i32 m0, %0, %1" :: "s"(lds_w), "n"(poff) : "m0");
       if constexpr (m < 64)
         mf(acc[i][j], xb[j], xa[i]);
       else
         mf(acc[i][j], yb[j], ya[i]);
       // Y.a: 16 halves at MFMAs 0-15
       if constexpr (m < 16) {
-        if constexpr (!(m & 1)) lo_y = rd_half(s_cur, m >> 1, 1, 0);
-        else ya[m >> 1] = join(lo_y, rd_half(s_cur, m >> 1, 1, 1));
+        if constexpr (!(m & 1)) lo_y = rd_half(ST, m >> 1, 1, 0);
+        else ya[m >> 1] = join(lo_y, rd_half(ST, m >> 1, 1, 1));
       }
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_t = tn_stamp();
       if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (pa) {
         if constexpr (TH_TN_M0SPLIT) piece_load(0, pi, pa2);
-        else piece_at(0, pi, pa2, st);
+        else piece_at(0, pi, pa2, ST);
       }
       // Y.b: 16 halves at MFMAs 23-38
       if constexpr (m >= 23 && m <= 38) {
         constexpr int h = m - 23;
-        if constexpr (!(h & 1)) lo_y = rd_half(s_cur, 8 + (h >> 1), 1, 0);
-        else yb[h >> 1] = join(lo_y, rd_half(s_cur, 8 + (h >> 1), 1, 1));
+        if constexpr (!(h & 1)) lo_y = rd_half(ST, 8 + (h >> 1), 1, 0);
+        else yb[h >> 1] = join(lo_y, rd_half(ST, 8 + (h >> 1), 1, 1));
       }
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (pb) {
         if constexpr (TH_TN_M0SPLIT) piece_load(1, pi, pb2);
-        else piece_at(1, pi, pb2, st);
+        else piece_at(1, pi, pb2, ST);
       }
       if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_w[m == 20 ? 0 : m == 44 ? 1 : 2] += tn_stamp() - d_t;
@@ -281,19 +282,33 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
         constexpr int ord[16] = {0, 8, 9, 10, 11, 12, 13, 14, 15, 1, 2, 3, 4, 5, 6, 7};
         constexpr int f = ord[h >> 1];
         if constexpr (!(h & 1)) {
-          lo_x = rd_half(s_nxt, f, 0, 0);
+          lo_x = rd_half(ST ^ 1, f, 0, 0);
         } else {
-          const bf16x8 v = join(lo_x, rd_half(s_nxt, f, 0, 1));
+          const bf16x8 v = join(lo_x, rd_half(ST ^ 1, f, 0, 1));
           if constexpr (f < 8) xa[f] = v;
           else xb[f - 8] = v;
         }
       }
       __builtin_amdgcn_sched_barrier(0);
     });
+  };
+  int t = 0;
+  auto advance = [&]() {  // k-tile t+2's first rows for the next k-tile's DMA
     if (t + 3 < nt) {
       pa2 += 64 * lda;
       pb2 += 64 * ldb;
     }
+    ++t;
+  };
+  for (; t + 1 < nt;) {
+    ktile(std::integral_constant<int, 0>{});
+    advance();
+    ktile(std::integral_constant<int, 1>{});
+    advance();
+  }
+  if (t < nt) {  // odd k-tile count: the last one sits in stage 0
+    ktile(std::integral_constant<int, 0>{});
+    advance();
   }
 #ifdef TH_TN_DIAG
   if (lane == 0) {

@@ -14,7 +14,8 @@ def _load():
 
 
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 64, 1), (512, 768, 1024, 1), (768, 512, 4096, 2),
-                                          (1024, 256, 2048, 4), (256, 1280, 640, 1)])
+                                          (1024, 256, 2048, 4), (256, 1280, 640, 1),
+                                          (512, 256, 192, 1), (256, 512, 1344, 1)])  # odd k-tile counts 3, 21
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("pingpong", [9, 10])
 def test_gemm_tn_matches_fp32(M, N, K, splitk, accumulate, pingpong):
