@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: TN loop unrolled per stage (production) vs the previous tree (diag_libs/tn_prev.so).
 set -o pipefail
-OUT=gpurun_out/r06/tnun
+OUT=gpurun_out/r06/tnun${TAG:+_$TAG}
 mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/gpu/test_gemm_tn_gpu.py > $OUT/pytest.log 2>&1; rc=$?; tail -2 $OUT/pytest.log; [ $rc = 0 ] || exit 1
 for i in 1 2 3; do

@@ -26,6 +26,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef TH_TN_GM
 #define TH_TN_GM 8  // output-tile rows per XCD band
 #endif
+#ifndef TH_TN_RSRC
+#define TH_TN_RSRC 1  // main-loop buffer descriptors as raw words advanced in place
+#endif
 #ifndef TH_TN_M0SPLIT
 // main-loop LDS-DMA pieces: M0 written before the gap's MFMA, load after it (307 -> 282 loop instructions;
 // wqkv / wo / w2 / w13 1.185 / 0.740 / 2.656 / 5.471 -> 1.168 / 0.732 / 2.614 / 5.417 ms, alternating processes
@@ -177,6 +180,16 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   // s_add straight into m0 BEFORE the MFMA of that gap, the buffer_load after it, so the MFMA is the
   // wait state the M0 write needs (no s_mov / s_nop per piece: 32 fewer scalar issues per k-tile)
   const unsigned lds_w = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)w * 1024u);
+  // TH_TN_RSRC: the main loop's buffer descriptors kept as raw words (base lo / hi advanced by one 32-bit
+  // add with carry per operand and k-tile) instead of a pointer advance + clamp + rebuilt descriptor
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  auto piece_load_w = [&](int op, int i, unsigned long long base) {
+    const long ld = op == 0 ? lda : ldb;
+    const i32x4 r = {(int)(unsigned)base, (int)(unsigned)(base >> 32), 0x7fffffff, 0x00020000};
+    const unsigned soff = (unsigned)(2L * 2 * (4 * i + w) * ld);
+    const unsigned voff = op == 0 ? va[i & 3] : vb[i & 3];
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(voff), "s"(r), "s"(soff) : "memory");
+  };
   auto piece_load = [&](int op, int i, const ushort* base) {
     const long ld = op == 0 ? lda : ldb;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
@@ -232,6 +245,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   // tile is re-staged (nobody reads it)
   const ushort* pa2 = ga + (long)min(2, nt - 1) * 64 * lda;
   const ushort* pb2 = gb + (long)min(2, nt - 1) * 64 * ldb;
+  unsigned long long ra2 = (unsigned long long)(uintptr_t)pa2, rb2 = (unsigned long long)(uintptr_t)pb2;
+  const unsigned step_a = 128u * (unsigned)lda, step_b = 128u * (unsigned)ldb;  // bytes per k-tile
   // k-tile t in stage ST = t & 1, unrolled per stage (two k-tiles per trip, plus an even tail tile)
   auto ktile = [&](auto stc) {
     constexpr int ST = decltype(stc)::value;
@@ -260,7 +275,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_t = tn_stamp();
       if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (pa) {
-        if constexpr (TH_TN_M0SPLIT) piece_load(0, pi, pa2);
+        if constexpr (TH_TN_M0SPLIT && TH_TN_RSRC) piece_load_w(0, pi, ra2);
+        else if constexpr (TH_TN_M0SPLIT) piece_load(0, pi, pa2);
         else piece_at(0, pi, pa2, ST);
       }
       // Y.b: 16 halves at MFMAs 23-38
@@ -271,7 +287,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       }
       if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (pb) {
-        if constexpr (TH_TN_M0SPLIT) piece_load(1, pi, pb2);
+        if constexpr (TH_TN_M0SPLIT && TH_TN_RSRC) piece_load_w(1, pi, rb2);
+        else if constexpr (TH_TN_M0SPLIT) piece_load(1, pi, pb2);
         else piece_at(1, pi, pb2, ST);
       }
       if constexpr (m == 88) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
@@ -294,7 +311,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
   };
   int t = 0;
   auto advance = [&]() {  // k-tile t+2's first rows for the next k-tile's DMA
-    if (t + 3 < nt) {
+    if constexpr (TH_TN_RSRC) {
+      const bool more = t + 3 < nt;  // past the end the last k-tile is re-staged (nobody reads it)
+      ra2 += more ? step_a : 0u;
+      rb2 += more ? step_b : 0u;
+    } else if (t + 3 < nt) {
       pa2 += 64 * lda;
       pb2 += 64 * ldb;
     }
