@@ -250,6 +250,9 @@ __device__ __forceinline__ void dma_kv_piece(const ushort* Kb, const ushort* Vb,
 #ifndef TH_FA_FWD_DEFAULT
 #define TH_FA_FWD_DEFAULT 15  // PRESCALE + DEFER + DMA-staged DBUF + KVMAJOR: 937 vs 829 TFLOP/s for 11 (B4 S4096, profiles/r01_flash_v3)
 #endif
+#ifndef TH_FA_FWD_RDORDER
+#define TH_FA_FWD_RDORDER 1
+#endif
 #ifndef TH_FA_FWD_AHEAD
 // K-row operand look-ahead of the forward S chain in k-steps (1 or 2).  2: fwd 1.047 / 1.055 vs 1.057 / 1.066 ms
 // (B 8 S 4096, alternating processes, profiles/r06_flash/ahead/), 200 instead of 220 VGPRs
@@ -368,6 +371,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         for (int t = 0; t < 2; ++t) {
           ka[t][0] = lds_row(ks, c32, 2 * t + h);
           ka[t][1] = lds_row(ks, 32 + c32, 2 * t + h);
+          if (TH_FA_FWD_RDORDER) __builtin_amdgcn_sched_barrier(0);  // issue order = use order: the first
+                                                                     // MFMA waits for its own operand only
         }
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
