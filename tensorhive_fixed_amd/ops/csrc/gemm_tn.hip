@@ -26,6 +26,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef TH_TN_GM
 #define TH_TN_GM 8  // output-tile rows per XCD band
 #endif
+#ifndef TH_TN_ONEBAR
+#define TH_TN_ONEBAR 0  // one WAR barrier per k-tile instead of two (A's and B's stage released together)
+#endif
 #ifndef TH_TN_RSRC
 #define TH_TN_RSRC 1  // main-loop buffer descriptors as raw words advanced in place
 #endif
@@ -256,7 +259,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       // DMA pieces spread over the whole k-tile: A's 8 every 4th MFMA from 22 (after the barrier that
       // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
       // (2 % faster than A every 2nd from 22 and B every 4th from 46: profiles/r05_gemm/tn_pv_sweep*.jsonl)
-      constexpr int a0 = 22, as = 4, b0 = 52, bs = 5;
+      // TH_TN_ONEBAR: Y.b read right after Y.a, ONE barrier (34) releases both operands' stage, then the DMA
+      constexpr int a0 = TH_TN_ONEBAR ? 36 : 22, as = TH_TN_ONEBAR ? 3 : 4, b0 = TH_TN_ONEBAR ? 59 : 52,
+                    bs = TH_TN_ONEBAR ? 4 : 5;
+      constexpr int yb0 = TH_TN_ONEBAR ? 16 : 23, bar1 = TH_TN_ONEBAR ? 34 : 20, bar2 = TH_TN_ONEBAR ? -1 : 44;
+      static_assert(a0 + 7 * as < b0 && b0 + 7 * bs < 88 && yb0 + 15 < bar1 + (TH_TN_ONEBAR ? 0 : 100), "TN slots");
       constexpr bool pa = m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0;
       constexpr bool pb = m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0;
       constexpr int pi = pa ? (m - a0) / as : (pb ? (m - b0) / bs : 0);
@@ -273,19 +280,19 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
         else ya[m >> 1] = join(lo_y, rd_half(ST, m >> 1, 1, 1));
       }
       if constexpr (kTnDiag && (m == 20 || m == 44 || m == 88)) d_t = tn_stamp();
-      if constexpr (m == 20) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (m == bar1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (pa) {
         if constexpr (TH_TN_M0SPLIT && TH_TN_RSRC) piece_load_w(0, pi, ra2);
         else if constexpr (TH_TN_M0SPLIT) piece_load(0, pi, pa2);
         else piece_at(0, pi, pa2, ST);
       }
       // Y.b: 16 halves at MFMAs 23-38
-      if constexpr (m >= 23 && m <= 38) {
-        constexpr int h = m - 23;
+      if constexpr (m >= yb0 && m <= yb0 + 15) {
+        constexpr int h = m - yb0;
         if constexpr (!(h & 1)) lo_y = rd_half(ST, 8 + (h >> 1), 1, 0);
         else yb[h >> 1] = join(lo_y, rd_half(ST, 8 + (h >> 1), 1, 1));
       }
-      if constexpr (m == 44) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if constexpr (m == bar2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if constexpr (pb) {
         if constexpr (TH_TN_M0SPLIT && TH_TN_RSRC) piece_load_w(1, pi, rb2);
         else if constexpr (TH_TN_M0SPLIT) piece_load(1, pi, pb2);
