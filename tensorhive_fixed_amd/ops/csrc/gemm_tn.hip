@@ -26,6 +26,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef TH_TN_GM
 #define TH_TN_GM 8  // output-tile rows per XCD band
 #endif
+#ifndef TH_TN_A0  // DMA piece slots: A's 8 at a0 + as * k (after the barrier at 20), B's at b0 + bs * k (after 44)
+#define TH_TN_A0 22
+#endif
+#ifndef TH_TN_AS
+#define TH_TN_AS 4
+#endif
+#ifndef TH_TN_B0
+#define TH_TN_B0 52
+#endif
+#ifndef TH_TN_BS
+#define TH_TN_BS 5
+#endif
 #ifndef TH_TN_ONEBAR
 #define TH_TN_ONEBAR 0  // one WAR barrier per k-tile instead of two (A's and B's stage released together)
 #endif
@@ -260,10 +272,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_hb_kernel(
       // releases A), B's 8 every 5th from 52 (after B's barrier at 44), the last one before the vmcnt at 88
       // (2 % faster than A every 2nd from 22 and B every 4th from 46: profiles/r05_gemm/tn_pv_sweep*.jsonl)
       // TH_TN_ONEBAR: Y.b read right after Y.a, ONE barrier (34) releases both operands' stage, then the DMA
-      constexpr int a0 = TH_TN_ONEBAR ? 36 : 22, as = TH_TN_ONEBAR ? 3 : 4, b0 = TH_TN_ONEBAR ? 59 : 52,
-                    bs = TH_TN_ONEBAR ? 4 : 5;
+      constexpr int a0 = TH_TN_ONEBAR ? 36 : TH_TN_A0, as = TH_TN_ONEBAR ? 3 : TH_TN_AS,
+                    b0 = TH_TN_ONEBAR ? 59 : TH_TN_B0, bs = TH_TN_ONEBAR ? 4 : TH_TN_BS;
       constexpr int yb0 = TH_TN_ONEBAR ? 16 : 23, bar1 = TH_TN_ONEBAR ? 34 : 20, bar2 = TH_TN_ONEBAR ? -1 : 44;
-      static_assert(a0 + 7 * as < b0 && b0 + 7 * bs < 88 && yb0 + 15 < bar1 + (TH_TN_ONEBAR ? 0 : 100), "TN slots");
+      static_assert(a0 > bar1 && a0 + 7 * as < b0 && b0 > (TH_TN_ONEBAR ? bar1 : bar2) && b0 + 7 * bs < 88 &&
+                    (TH_TN_ONEBAR == 0 || yb0 + 15 < bar1), "TN DMA slots");
       constexpr bool pa = m >= a0 && m < a0 + 8 * as && (m - a0) % as == 0;
       constexpr bool pb = m >= b0 && m < b0 + 8 * bs && (m - b0) % bs == 0;
       constexpr int pi = pa ? (m - a0) / as : (pb ? (m - b0) / bs : 0);
