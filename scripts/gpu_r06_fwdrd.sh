@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 6: forward S-chain operand read order (production: step-0 reads issued first) vs diag_libs/fwd_rd0.so.
+# Round 6: forward kernel change (production) vs diag_libs/fwd_rd0.so (the previous form), alternating processes.
 set -o pipefail
-OUT=gpurun_out/r06/fwdrd
+OUT=gpurun_out/r06/fwdrd${TAG:+_$TAG}
 mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/gpu/test_flash_attn_gpu.py > $OUT/pytest.log 2>&1; rc=$?; tail -2 $OUT/pytest.log; [ $rc = 0 ] || exit 1
 export B=8 NO_BWD=1 VARIANTS=15,15
