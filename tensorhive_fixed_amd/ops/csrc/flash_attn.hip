@@ -838,6 +838,9 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_pp_kernel(
 #ifndef TH_DQ_AHEAD
 #define TH_DQ_AHEAD 1  // 0: reads issued right before their MFMA (compiler order)
 #endif
+#ifndef TH_DQ_PREKB
+#define TH_DQ_PREKB 1
+#endif
 #ifndef TH_DQ_TR_AHEAD
 #define TH_DQ_TR_AHEAD 1  // K^T operand look-ahead of the dQ chain in d-steps (1 or 2)
 #endif
@@ -950,6 +953,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
       continue;
     }
     const bool need_mask = (causal && kbase + F_BN - 1 > q0) || (kbase + F_BN > S);
+    // TH_DQ_PREKB: the second key half's first S|dP operands are read during the first half's dQ chain
+    bf16x8 pka[2], pva[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {  // 32-key halves: keeps only one S^T / dP^T pair live
       f32x16 sacc = s_init, pacc = p_init;
@@ -958,8 +963,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
         bf16x8 ka[2], va[2];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          ka[s] = lds_row(ks, 32 * kb + c32, 2 * s + h);
-          va[s] = lds_row(vs, 32 * kb + c32, 2 * s + h);
+          if (TH_DQ_PREKB && DMA && kb == 1) {
+            ka[s] = pka[s];
+            va[s] = pva[s];
+          } else {
+            ka[s] = lds_row(ks, 32 * kb + c32, 2 * s + h);
+            va[s] = lds_row(vs, 32 * kb + c32, 2 * s + h);
+          }
         }
         TH_DQ_PRIO(1);
 #pragma unroll
@@ -1035,6 +1045,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
           if (d < 3) {
             n0 = lds_tr(ks, 32 * kb, 32 * d + 32, lane);
             n1 = lds_tr(ks, 32 * kb + 16, 32 * d + 32, lane);
+          }
+          if (TH_DQ_PREKB && DMA && kb == 0 && d == 2) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              pka[s] = lds_row(ks, 32 + c32, 2 * s + h);
+              pva[s] = lds_row(vs, 32 + c32, 2 * s + h);
+            }
           }
           __builtin_amdgcn_sched_barrier(0);
           dq[d] = mfma(t0, s0, dq[d]);
