@@ -1624,6 +1624,9 @@ __device__ __forceinline__ unsigned long long kf_stamp() { return 0; }
 __device__ __forceinline__ void kf_stamp_add(int, unsigned long long) {}
 #endif
 #define BAR_OF(V) (((V) & 64) ? 0 : 48)
+#ifndef TH_KF_WAIT2
+#define TH_KF_WAIT2 1
+#endif
 
 // one 128-key block (keys kblk0 ..) of (batch b, kv head hk)
 template <int VAR>
@@ -1841,6 +1844,9 @@ __device__ __forceinline__ void kf_block(
       constexpr int ni = i + PD;
       const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
       __builtin_amdgcn_sched_barrier(0);
+      // TH_KF_WAIT2: one lgkmcnt(2) per MFMA pair (a wait the compiler's waitcnt pass sees) instead of one
+      // per MFMA: the pair's operands, read 3 and 2 MFMAs ahead, are older than the two newest reads
+      if constexpr (TH_KF_WAIT2 && (i & 1) == 0) __builtin_amdgcn_s_waitcnt(0xC27F);
       const bf16x8 a = opr[i % NR];
       constexpr bool pad = !(VAR & 8) || i == 0 || i == 16 || i == 32 || i == 33 || i == 48 || i == 49;
       if constexpr (i < 32) {
