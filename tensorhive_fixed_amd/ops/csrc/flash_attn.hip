@@ -1624,6 +1624,9 @@ __device__ __forceinline__ unsigned long long kf_stamp() { return 0; }
 __device__ __forceinline__ void kf_stamp_add(int, unsigned long long) {}
 #endif
 #define BAR_OF(V) (((V) & 64) ? 0 : 48)
+#ifndef TH_KF_M0SPLIT
+#define TH_KF_M0SPLIT 1
+#endif
 #ifndef TH_KF_WAIT2
 #define TH_KF_WAIT2 1
 #endif
@@ -1713,6 +1716,22 @@ __device__ __forceinline__ void kf_block(
       const unsigned r = rc[u - 1];
       const int row = d_qq0 + (int)(r & 255);
       glds16(d_base, (unsigned)(row * d_ldx + (r >> 8) * 8) * 2u, d_img + (u - 1) * 1024);
+    }
+  };
+  // TH_KF_M0SPLIT: a gap's piece in two halves -- M0 before the gap's MFMA, the load after it, so the MFMA
+  // is the wait state the M0 write needs (no s_nop per piece; the TN kernel's round-6 cut)
+  auto dma_m0 = [&](int u) {
+    const unsigned lds = u == 0 ? d_slot0 + 2 * C_BQ * 256 + w * (C_BQ * 4) : d_img + (u - 1) * 1024;
+    asm volatile("s_mov_b32 m0, %0" :: "s"(lds) : "m0");
+  };
+  auto dma_load = [&](int u) {
+    if (u == 0) {
+      asm volatile("global_load_lds_dword %0, %1" :: "v"((unsigned)lane * 4u), "s"(d_lb) : "memory");
+    } else {
+      const unsigned r = rc[u - 1];
+      const int row = d_qq0 + (int)(r & 255);
+      asm volatile("global_load_lds_dwordx4 %0, %1" :: "v"((unsigned)(row * d_ldx + (r >> 8) * 8) * 2u), "s"(d_base)
+                   : "memory");
     }
   };
   auto dma_tile = [&](int j, int slot) {
@@ -1840,7 +1859,10 @@ __device__ __forceinline__ void kf_block(
         else
           dma_tile(it + 2, (it + 2) % KF_STAGES);
       }
-      if constexpr ((VAR & 4) && i >= BAR && i < BAR + 9) dma_piece(i - BAR);
+      if constexpr ((VAR & 4) && i >= BAR && i < BAR + 9) {
+        if constexpr (TH_KF_M0SPLIT) dma_m0(i - BAR);
+        else dma_piece(i - BAR);
+      }
       constexpr int ni = i + PD;
       const bf16x8 nx = ni < 64 ? opnd(ni, cur) : opnd(ni - 64, nxt);
       __builtin_amdgcn_sched_barrier(0);
@@ -1857,6 +1879,10 @@ __device__ __forceinline__ void kf_block(
         constexpr int r = (i - 32) & 15, kb = (i - 32) >> 4, d = r >> 2, sub = r & 3;
         if constexpr (sub < 2) mfma_a<pad>(av[d], a, pp[kb][sub]);
         else mfma_a<pad>(ak[d], a, sp[kb][sub & 1]);
+      }
+      if constexpr (TH_KF_M0SPLIT && (VAR & 4) && i >= BAR && i < BAR + 9) {
+        __builtin_amdgcn_sched_barrier(0);  // the MFMA stays between the M0 write and the load
+        dma_load(i - BAR);
       }
       // VALU of the gap
       if constexpr (i == 16 || i == 32) {
